@@ -1,0 +1,495 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the reference's paged-attention decode path and of the
+// INT8Decoder layer maths.  Only tests/, bench.py's
+// cpu_baseline leg and __graft_entry__.smoke() may load this library, and only
+// as the checker / CPU baseline.  The product path (the HIP library under
+// pagedattention-based-transformer-decoder-inference-framework_amd/csrc) never
+// links or calls it.
+//
+// Parity pinning: the attention / softmax / quantizer / LayerNorm / MLP pieces
+// below are checked against golden vectors produced by
+// oracle/ref_golden/gen_golden.cpp, which links the reference's own compilable
+// sources (kv_tile_cache_cpu.cpp, softmax_lut.cpp, int8_quant.cpp, mlp.hpp,
+// layer_norm.hpp) — see tests/test_oracle_golden.py.  The INT8 GEMM contract
+// (oneDNN, not vendored) is "parity unpinned" beyond the exact int32
+// accumulator, which is cross-checked against torch._int_mm.
+//
+// Reference citations are relative to the reference tree root.
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <utility>
+#include <vector>
+#include <omp.h>
+
+namespace {
+
+// Exact IEEE binary16 -> binary32 (no F16C dependency).
+inline float half_to_float(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  uint32_t exp = (h >> 10) & 0x1Fu;
+  uint32_t mant = h & 0x3FFu;
+  uint32_t bits;
+  if (exp == 0) {
+    if (mant == 0) {
+      bits = sign;
+    } else {  // subnormal: renormalise
+      exp = 127 - 15 + 1;
+      while ((mant & 0x400u) == 0) { mant <<= 1; --exp; }
+      mant &= 0x3FFu;
+      bits = sign | (exp << 23) | (mant << 13);
+    }
+  } else if (exp == 31) {
+    bits = sign | 0x7F800000u | (mant << 13);
+  } else {
+    bits = sign | ((exp + 127 - 15) << 23) | (mant << 13);
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+
+// binary32 -> binary16, round to nearest even (matches __float2half_rn and
+// numpy.float16).
+inline uint16_t float_to_half(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t absx = x & 0x7FFFFFFFu;
+  if (absx >= 0x7F800000u) {  // inf / nan
+    return (uint16_t)(sign | 0x7C00u | (absx > 0x7F800000u ? 0x200u : 0));
+  }
+  if (absx >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);  // overflow -> inf
+  if (absx < 0x33000001u) return (uint16_t)sign;                // underflow -> 0
+  int e = (int)(absx >> 23) - 127;
+  uint32_t m = (absx & 0x7FFFFFu) | 0x800000u;
+  if (e < -14) {  // subnormal half
+    const int shift = -14 - e + 13;
+    uint32_t r = m >> shift;
+    const uint32_t rem = m & ((1u << shift) - 1);
+    const uint32_t halfway = 1u << (shift - 1);
+    if (rem > halfway || (rem == halfway && (r & 1u))) ++r;
+    return (uint16_t)(sign | r);
+  }
+  uint32_t r = m >> 13;
+  const uint32_t rem = m & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (r & 1u))) ++r;
+  uint32_t he = (uint32_t)(e + 15);
+  if (r & 0x800u) { r >>= 1; ++he; }
+  if (he >= 31) return (uint16_t)(sign | 0x7C00u);
+  return (uint16_t)(sign | (he << 10) | (r & 0x3FFu));
+}
+
+// softmax_lut_vec restated (attention_cpu/softmax_lut.cpp:203-231): max over
+// the scores, x = (s - max) / temperature, exp, block-of-8 partial sums, then
+// multiply by 1 / (sum + 1e-6).  The reference requires len % 8 == 0; the
+// restatement also handles a ragged tail the same way (blocks of up to 8).
+void softmax_vec(const float* scores, int len, float temperature, float* out) {
+  float maxval = -1e9f;
+  for (int i = 0; i < len; ++i) maxval = std::max(maxval, scores[i]);
+  float sum = 0.0f;
+  for (int i = 0; i < len; i += 8) {
+    float blk = 0.0f;
+    const int n = std::min(8, len - i);
+    for (int j = 0; j < n; ++j) {
+      const float x = std::exp((scores[i + j] - maxval) / temperature);
+      out[i + j] = x;
+      blk += x;
+    }
+    sum += blk;
+  }
+  const float inv = 1.0f / (sum + 1e-6f);
+  for (int i = 0; i < len; ++i) out[i] = out[i] * inv;
+}
+
+// apply_topk_topp_filter restated (attention_cpu/softmax_lut.cpp:233-256):
+// stable descending sort of (prob, index), zero everything past top_k or past
+// cumulative top_p, no renormalisation; optional EOS hard threshold.
+void topk_topp_filter(float* probs, int len, int top_k, float top_p, int eos, float eos_thr) {
+  if (top_k <= 0 && top_p >= 1.0f && eos < 0) return;
+  std::vector<std::pair<float, int>> sorted;
+  sorted.reserve(len);
+  for (int i = 0; i < len; ++i) sorted.emplace_back(probs[i], i);
+  std::sort(sorted.begin(), sorted.end(), std::greater<>());
+  float cum = 0.0f;
+  for (int i = 0; i < len; ++i) {
+    const int idx = sorted[i].second;
+    if ((top_k > 0 && i >= top_k) || (top_p < 1.0f && cum >= top_p)) probs[idx] = 0.0f;
+    cum += sorted[i].first;
+  }
+  if (eos >= 0 && eos < len && probs[eos] > eos_thr)
+    for (int i = 0; i < len; ++i)
+      if (i != eos) probs[i] = 0.0f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int oracle_version() { return 1; }
+
+void oracle_half_to_float(const uint16_t* in, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = half_to_float(in[i]);
+}
+
+void oracle_float_to_half(const float* in, uint16_t* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = float_to_half(in[i]);
+}
+
+// PageTable::index / lookup restated (kv_cache/page_table.hpp:39-49):
+// idx = beam * (H * NT) + head * NT + tile; out of range -> -1.
+int oracle_page_lookup(const int32_t* table, int num_beams, int num_heads, int num_tiles,
+                       int beam, int head, int tile) {
+  const int64_t total = (int64_t)num_beams * num_heads * num_tiles;
+  const int64_t idx = (int64_t)beam * (num_heads * num_tiles) + (int64_t)head * num_tiles + tile;
+  if (idx < 0 || idx >= total) return -1;
+  if (tile < 0 || tile >= num_tiles || head < 0 || head >= num_heads) return -1;
+  return table[idx];
+}
+
+// cpu_paged_attention_forward restated (attention_cpu/cpu_attention_kernel.cpp:37-129).
+//   * beam routing: beam = beam_ids ? beam_ids[b] : b                    (:50)
+//   * scores[T] initialised to -1e9                                       (:61)
+//   * tile walk, missing tile skipped, partial last tile                  (:68-86)
+//   * score = dot(q, k_t) / temperature, decode query sees all keys       (:85; Appendix A #12)
+//   * softmax_lut_vec (divides by temperature again)                      (softmax_lut.cpp:203-231)
+//   * apply_topk_topp_filter                                              (softmax_lut.cpp:233-256)
+//   * out = sum_t p_t v_t over present tiles                              (:103-117)
+// KVTileCache<T>::get (kv_cache/kv_tile_cache.hpp:21-26): page < 0 or
+// page >= num_pages -> no tile; else pool + page * ts * D.
+// context_lens (nullable) gives a per-row T_b <= T (ragged batches).
+int oracle_paged_attention(const float* q, const float* k_pool, const float* v_pool,
+                           const int32_t* page_table, int num_pages, int ts, int num_beams,
+                           int max_tiles, const int32_t* beam_ids, const int32_t* context_lens,
+                           int B, int H, int D, int T, float temperature, int top_k, float top_p,
+                           int eos_token, float eos_threshold, float* out, float* probs_out,
+                           float* scores_out) {
+  if (B < 0 || H <= 0 || D <= 0 || T < 0 || ts <= 0) return 1;
+#pragma omp parallel for collapse(2) schedule(dynamic)
+  for (int b = 0; b < B; ++b) {
+    for (int h = 0; h < H; ++h) {
+      const int beam = beam_ids ? beam_ids[b] : b;
+      const int Tb = context_lens ? std::min(context_lens[b], T) : T;
+      const int ntiles = (Tb + ts - 1) / ts;
+      const float* qv = q + ((int64_t)b * H + h) * D;
+      std::vector<float> scores(std::max(Tb, 1), -1e9f);
+      std::vector<float> probs(std::max(Tb, 1), 0.0f);
+      std::vector<const float*> ktile(ntiles, nullptr), vtile(ntiles, nullptr);
+      for (int tile = 0; tile < ntiles; ++tile) {
+        const int page = oracle_page_lookup(page_table, num_beams, H, max_tiles, beam, h, tile);
+        if (page < 0 || page >= num_pages) continue;
+        ktile[tile] = k_pool + (int64_t)page * ts * D;
+        vtile[tile] = v_pool + (int64_t)page * ts * D;
+      }
+      for (int tile = 0; tile < ntiles; ++tile) {
+        const int start = tile * ts;
+        const int len = std::min(ts, Tb - start);
+        const float* kt = ktile[tile];
+        if (!kt) continue;
+        for (int t = 0; t < len; ++t) {
+          float dot = 0.0f;
+          for (int d = 0; d < D; ++d) dot += qv[d] * kt[(int64_t)t * D + d];
+          scores[start + t] = dot / temperature;
+        }
+      }
+      float* o = out + ((int64_t)b * H + h) * D;
+      for (int d = 0; d < D; ++d) o[d] = 0.0f;
+      if (Tb > 0) {
+        softmax_vec(scores.data(), Tb, temperature, probs.data());
+        topk_topp_filter(probs.data(), Tb, top_k, top_p, eos_token, eos_threshold);
+        for (int tile = 0; tile < ntiles; ++tile) {
+          const int start = tile * ts;
+          const int len = std::min(ts, Tb - start);
+          const float* vt = vtile[tile];
+          if (!vt) continue;
+          for (int t = 0; t < len; ++t) {
+            const float p = probs[start + t];
+            for (int d = 0; d < D; ++d) o[d] += p * vt[(int64_t)t * D + d];
+          }
+        }
+      }
+      if (probs_out) {
+        float* po = probs_out + ((int64_t)b * H + h) * T;
+        for (int t = 0; t < T; ++t) po[t] = t < Tb ? probs[t] : 0.0f;
+      }
+      if (scores_out) {
+        float* so = scores_out + ((int64_t)b * H + h) * T;
+        for (int t = 0; t < T; ++t) so[t] = t < Tb ? scores[t] : -1e9f;
+      }
+    }
+  }
+  return 0;
+}
+
+// compute_minmax_scale (attention_cpu/int8_quant.cpp:59-64):
+// scale = 127 / (max(|min|, |max|) + 1e-6).
+float oracle_minmax_scale(const float* x, int64_t n) {
+  float mn = x[0], mx = x[0];
+  for (int64_t i = 1; i < n; ++i) { mn = std::min(mn, x[i]); mx = std::max(mx, x[i]); }
+  const float absmax = std::max(std::fabs(mn), std::fabs(mx));
+  return 127.f / (absmax + 1e-6f);
+}
+
+// quantize_to_int8 (attention_cpu/int8_quant.cpp:5-13): q = clamp(round(x*scale)).
+void oracle_quantize(const float* x, int64_t n, float scale, int8_t* q) {
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t v = (int32_t)std::round(x[i] * scale);
+    v = std::max(-128, std::min(127, v));
+    q[i] = (int8_t)v;
+  }
+}
+
+// Per-row dynamic activation quantisation (batch_quantize, int8_quant.cpp:15-28,
+// with the per-row scale of compute_minmax_scale).  inv_scale[r] = 1 / scale_r
+// is the dequant multiplier (dequantize_from_int8 divides by scale, :38-44).
+void oracle_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv_scale) {
+  for (int r = 0; r < rows; ++r) {
+    const float scale = oracle_minmax_scale(x + (int64_t)r * cols, cols);
+    oracle_quantize(x + (int64_t)r * cols, cols, scale, q + (int64_t)r * cols);
+    inv_scale[r] = 1.0f / scale;
+  }
+}
+
+// Per-output-column weight quantisation of W[K][N] (the INT8 weight format of
+// this build; one scale per output channel, int8_quant.cpp semantics).
+void oracle_quantize_cols(const float* w, int K, int N, int8_t* q, float* inv_scale) {
+  std::vector<float> col(K);
+  for (int n = 0; n < N; ++n) {
+    for (int k = 0; k < K; ++k) col[k] = w[(int64_t)k * N + n];
+    const float scale = oracle_minmax_scale(col.data(), K);
+    for (int k = 0; k < K; ++k) {
+      int32_t v = (int32_t)std::round(col[k] * scale);
+      v = std::max(-128, std::min(127, v));
+      q[(int64_t)k * N + n] = (int8_t)v;
+    }
+    inv_scale[n] = 1.0f / scale;
+  }
+}
+
+// INT8 GEMM contract (attention_cpu/dnnl_matmul_int8.cpp:7-75):
+//   acc[m,n] = sum_k int32(A[m,k]) * int32(W[k,n])            (exact)
+//   y = float(acc) * (sa[m] * sw[n]) + bias[n]; act in {0 none, 1 relu, 2 gelu_erf}
+// A: [M][K] row-major, W: [K][N] row-major (mlp.hpp:28-31 layout).
+void oracle_i8_gemm(const int8_t* A, const int8_t* W, int32_t* acc_out, float* C, int M, int N,
+                    int K, const float* sa, const float* sw, const float* bias, int act) {
+#pragma omp parallel
+  {
+    std::vector<int32_t> acc(N);
+#pragma omp for schedule(static)
+    for (int m = 0; m < M; ++m) {
+      std::fill(acc.begin(), acc.end(), 0);
+      const int8_t* a = A + (int64_t)m * K;
+      for (int k = 0; k < K; ++k) {
+        const int32_t av = a[k];
+        if (av == 0) continue;
+        const int8_t* w = W + (int64_t)k * N;
+        for (int n = 0; n < N; ++n) acc[n] += av * (int32_t)w[n];
+      }
+      if (acc_out) std::memcpy(acc_out + (int64_t)m * N, acc.data(), sizeof(int32_t) * N);
+      if (C) {
+        const float sam = sa ? sa[m] : 1.0f;
+        for (int n = 0; n < N; ++n) {
+          const float s = sam * (sw ? sw[n] : 1.0f);
+          float y = (float)acc[n] * s;
+          if (bias) y = y + bias[n];
+          if (act == 1) y = std::max(0.0f, y);
+          else if (act == 2) y = 0.5f * y * (1.0f + std::erf(y * 0.70710678118654752f));
+          C[(int64_t)m * N + n] = y;
+        }
+      }
+    }
+  }
+}
+
+// LayerNorm<T>::forward restated (decoder/layer_norm.hpp:20-37), T = float:
+// sequential mean, biased variance, inv_std = 1.0 / sqrt(var + eps) (double
+// division of the float sqrt, as written), out = (x-mean)*inv_std*g + b.
+void oracle_layer_norm(const float* x, int rows, int cols, const float* gamma, const float* beta,
+                       float eps, float* out) {
+  for (int r = 0; r < rows; ++r) {
+    const float* in = x + (int64_t)r * cols;
+    float* o = out + (int64_t)r * cols;
+    float mean = 0;
+    for (int j = 0; j < cols; ++j) mean += in[j];
+    mean /= cols;
+    float var = 0;
+    for (int j = 0; j < cols; ++j) var += (in[j] - mean) * (in[j] - mean);
+    var /= cols;
+    const float inv_std = (float)(1.0 / std::sqrt(var + eps));
+    for (int j = 0; j < cols; ++j) o[j] = (in[j] - mean) * inv_std * gamma[j] + beta[j];
+  }
+}
+
+// MLP<float>::forward restated (decoder/mlp.hpp:23-41): fc1 [hid][inter]
+// row-major + bias, ReLU, fc2 [inter][hid] + bias, float accumulation in
+// index order starting from the bias.
+void oracle_mlp_f32(const float* x, int rows, int hid, int inter, const float* w1, const float* b1,
+                    const float* w2, const float* b2, float* out) {
+  std::vector<float> h(inter);
+  for (int b = 0; b < rows; ++b) {
+    for (int i = 0; i < inter; ++i) {
+      float sum = b1[i];
+      for (int j = 0; j < hid; ++j) sum += x[(int64_t)b * hid + j] * w1[(int64_t)j * inter + i];
+      h[i] = std::max(0.0f, sum);
+    }
+    for (int i = 0; i < hid; ++i) {
+      float sum = b2[i];
+      for (int j = 0; j < inter; ++j) sum += h[j] * w2[(int64_t)j * hid + i];
+      out[(int64_t)b * hid + i] = sum;
+    }
+  }
+}
+
+// sample_from_logits (decoder/cuda_decoder.cu:7-14): argmax of logits/temperature,
+// first maximum wins (std::max_element).
+void oracle_argmax_rows(const float* logits, int rows, int V, int32_t* out) {
+  for (int r = 0; r < rows; ++r) {
+    const float* l = logits + (int64_t)r * V;
+    out[r] = (int32_t)(std::max_element(l, l + V) - l);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Restated INT8Decoder decode step (reference order of
+// decoder/decoder_block.hpp:41-62 plus the BUILD DECISION projections):
+//   x = E[id]
+//   per layer: a = LN1(x); qkv = i8gemm(quant(a), Wqkv); append k,v (fp16);
+//              o = attn(q) over positions [0, pos]; x = i8gemm(quant(o), Wo);
+//              a2 = LN2(x); h = relu(i8gemm(quant(a2), W1) + b1);
+//              x = i8gemm(quant(h), W2) + b2
+//   logits = x . E^T (fp16 E, double accumulation); next = argmax.
+// The KV cache is contiguous per (layer, row, head) here (no paging): the
+// paging itself is pinned separately by oracle_paged_attention.
+// ---------------------------------------------------------------------------
+struct oracle_model {
+  int L, H, D, hid, inter, V, max_seq;
+  const uint16_t* emb;                 // [V][hid] fp16 bits
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;  // [L][hid]
+  const int8_t* wqkv; const float* sw_qkv;     // [L][hid][3hid], [L][3hid]
+  const int8_t* wo;   const float* sw_o;       // [L][hid][hid],  [L][hid]
+  const int8_t* w1;   const float* sw1; const float* b1;  // [L][hid][inter], [L][inter] x2
+  const int8_t* w2;   const float* sw2; const float* b2;  // [L][inter][hid], [L][hid] x2
+};
+
+struct OracleDecoder {
+  oracle_model m;
+  int B;
+  std::vector<uint16_t> k, v;  // [L][B][H][max_seq][D] fp16 bits
+  int64_t kv_index(int l, int b, int h, int t) const {
+    return ((((int64_t)l * B + b) * m.H + h) * m.max_seq + t) * m.D;
+  }
+};
+
+void* oracle_decoder_create(const oracle_model* model, int B) {
+  auto* d = new OracleDecoder();
+  d->m = *model;
+  d->B = B;
+  const size_t n = (size_t)model->L * B * model->H * model->max_seq * model->D;
+  d->k.assign(n, 0);
+  d->v.assign(n, 0);
+  return d;
+}
+
+void oracle_decoder_destroy(void* h) { delete static_cast<OracleDecoder*>(h); }
+
+uint16_t* oracle_decoder_kv_ptr(void* h, int layer, int which) {
+  auto* d = static_cast<OracleDecoder*>(h);
+  return (which == 0 ? d->k.data() : d->v.data()) + d->kv_index(layer, 0, 0, 0);
+}
+
+// One decode step for all B rows.  tokens[b] is the token at position pos[b];
+// attention covers positions [0, pos[b]].  Runs the first `layers_to_run`
+// layers (all if < 0) and the LM head + argmax if do_lm_head.
+int oracle_decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
+                        int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
+                        int32_t* next_out) {
+  auto* d = static_cast<OracleDecoder*>(handle);
+  const oracle_model& m = d->m;
+  const int B = d->B, H = m.H, D = m.D, hid = m.hid, inter = m.inter;
+  for (int b = 0; b < B; ++b)
+    if (pos[b] < 0 || pos[b] >= m.max_seq || tokens[b] < 0 || tokens[b] >= m.V) return 2;
+  const int Lrun = layers_to_run < 0 ? m.L : std::min(layers_to_run, m.L);
+  std::vector<float> x((size_t)B * hid), a((size_t)B * hid), qkv((size_t)B * 3 * hid),
+      o((size_t)B * hid), h1((size_t)B * inter);
+  std::vector<int8_t> qa((size_t)B * std::max(hid, inter));
+  std::vector<float> sa(B);
+  for (int b = 0; b < B; ++b)
+    for (int j = 0; j < hid; ++j) x[(size_t)b * hid + j] = half_to_float(m.emb[(size_t)tokens[b] * hid + j]);
+
+  for (int l = 0; l < Lrun; ++l) {
+    const size_t lh = (size_t)l * hid;
+    oracle_layer_norm(x.data(), B, hid, m.ln1_g + lh, m.ln1_b + lh, 1e-5f, a.data());
+    oracle_quantize_rows(a.data(), B, hid, qa.data(), sa.data());
+    oracle_i8_gemm(qa.data(), m.wqkv + (size_t)l * hid * 3 * hid, nullptr, qkv.data(), B, 3 * hid,
+                   hid, sa.data(), m.sw_qkv + (size_t)l * 3 * hid, nullptr, 0);
+    // KV append (fp16 storage, round to nearest even).
+    for (int b = 0; b < B; ++b)
+      for (int hh = 0; hh < H; ++hh)
+        for (int dd = 0; dd < D; ++dd) {
+          const size_t idx = d->kv_index(l, b, hh, pos[b]) + dd;
+          d->k[idx] = float_to_half(qkv[(size_t)b * 3 * hid + hid + hh * D + dd]);
+          d->v[idx] = float_to_half(qkv[(size_t)b * 3 * hid + 2 * hid + hh * D + dd]);
+        }
+    // Attention: the reference scores are dot/temperature and its softmax divides
+    // by temperature again (Appendix A #13); attn_scale = 1/temperature^2 folds
+    // both.  exp(s - max) / (sum + 1e-6), out = sum p v.
+#pragma omp parallel for collapse(2) schedule(dynamic)
+    for (int b = 0; b < B; ++b) {
+      for (int hh = 0; hh < H; ++hh) {
+        const int Tb = pos[b] + 1;
+        const float* qv = qkv.data() + (size_t)b * 3 * hid + hh * D;
+        std::vector<float> sc(Tb), pr(Tb);
+        const size_t base = d->kv_index(l, b, hh, 0);
+        std::vector<float> kf(D);
+        for (int t = 0; t < Tb; ++t) {
+          const uint16_t* kr = d->k.data() + base + (size_t)t * D;
+          float dot = 0.0f;
+          for (int dd = 0; dd < D; ++dd) dot += qv[dd] * half_to_float(kr[dd]);
+          sc[t] = dot * attn_scale;
+        }
+        softmax_vec(sc.data(), Tb, 1.0f, pr.data());
+        float* ov = o.data() + (size_t)b * hid + hh * D;
+        for (int dd = 0; dd < D; ++dd) ov[dd] = 0.0f;
+        for (int t = 0; t < Tb; ++t) {
+          const uint16_t* vr = d->v.data() + base + (size_t)t * D;
+          const float p = pr[t];
+          for (int dd = 0; dd < D; ++dd) ov[dd] += p * half_to_float(vr[dd]);
+        }
+      }
+    }
+    oracle_quantize_rows(o.data(), B, hid, qa.data(), sa.data());
+    oracle_i8_gemm(qa.data(), m.wo + (size_t)l * hid * hid, nullptr, x.data(), B, hid, hid,
+                   sa.data(), m.sw_o + lh, nullptr, 0);
+    oracle_layer_norm(x.data(), B, hid, m.ln2_g + lh, m.ln2_b + lh, 1e-5f, a.data());
+    oracle_quantize_rows(a.data(), B, hid, qa.data(), sa.data());
+    oracle_i8_gemm(qa.data(), m.w1 + (size_t)l * hid * inter, nullptr, h1.data(), B, inter, hid,
+                   sa.data(), m.sw1 + (size_t)l * inter, m.b1 + (size_t)l * inter, 1);
+    oracle_quantize_rows(h1.data(), B, inter, qa.data(), sa.data());
+    oracle_i8_gemm(qa.data(), m.w2 + (size_t)l * inter * hid, nullptr, x.data(), B, hid, inter,
+                   sa.data(), m.sw2 + lh, m.b2 + lh, 0);
+  }
+  if (x_out) std::memcpy(x_out, x.data(), sizeof(float) * x.size());
+  if (!do_lm_head) return 0;
+  std::vector<float> logits((size_t)B * m.V);
+#pragma omp parallel for schedule(static)
+  for (int vv = 0; vv < m.V; ++vv) {
+    const uint16_t* e = m.emb + (size_t)vv * hid;
+    for (int b = 0; b < B; ++b) {
+      double acc = 0.0;
+      const float* xb = x.data() + (size_t)b * hid;
+      for (int j = 0; j < hid; ++j) acc += (double)xb[j] * (double)half_to_float(e[j]);
+      logits[(size_t)b * m.V + vv] = (float)acc;
+    }
+  }
+  if (logits_out) std::memcpy(logits_out, logits.data(), sizeof(float) * logits.size());
+  if (next_out) oracle_argmax_rows(logits.data(), B, m.V, next_out);
+  return 0;
+}
+
+int oracle_num_threads() { return omp_get_max_threads(); }
+
+}  // extern "C"

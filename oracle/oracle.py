@@ -1,0 +1,291 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes front-end for ``oracle/liboracle.so`` (the C++/OpenMP restatement of the
+reference's paged-attention decode path and INT8Decoder layer maths, see
+``oracle.cpp``) plus small numpy helpers shared by the tests and bench.py's
+``cpu_baseline`` leg.  Nothing in the product package imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i8p = ctypes.POINTER(ctypes.c_int8)
+_u16p = ctypes.POINTER(ctypes.c_uint16)
+
+
+def build(force: bool = False) -> None:
+    """Compile oracle/liboracle*.so (gcc, no GPU needed)."""
+    libs = [HERE / "liboracle.so", HERE / "liboracle_bench.so"]
+    if force or not all(p.exists() for p in libs) or any(
+        p.stat().st_mtime < (HERE / "oracle.cpp").stat().st_mtime for p in libs
+    ):
+        subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+class OracleModel(ctypes.Structure):
+    _fields_ = [
+        ("L", ctypes.c_int), ("H", ctypes.c_int), ("D", ctypes.c_int), ("hid", ctypes.c_int),
+        ("inter", ctypes.c_int), ("V", ctypes.c_int), ("max_seq", ctypes.c_int),
+        ("emb", _u16p),
+        ("ln1_g", _f32p), ("ln1_b", _f32p), ("ln2_g", _f32p), ("ln2_b", _f32p),
+        ("wqkv", _i8p), ("sw_qkv", _f32p),
+        ("wo", _i8p), ("sw_o", _f32p),
+        ("w1", _i8p), ("sw1", _f32p), ("b1", _f32p),
+        ("w2", _i8p), ("sw2", _f32p), ("b2", _f32p),
+    ]
+
+
+def _ptr(a: np.ndarray | None, typ):
+    if a is None:
+        return ctypes.cast(None, typ)
+    assert a.flags["C_CONTIGUOUS"], "oracle arrays must be C-contiguous"
+    return a.ctypes.data_as(typ)
+
+
+class Oracle:
+    def __init__(self, bench: bool = False):
+        build()
+        name = "liboracle_bench.so" if bench else "liboracle.so"
+        self.lib = ctypes.CDLL(str(HERE / name))
+        L = self.lib
+        L.oracle_paged_attention.restype = ctypes.c_int
+        L.oracle_paged_attention.argtypes = [
+            _f32p, _f32p, _f32p, _i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+            _i32p, _i32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+            ctypes.c_float, ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_float,
+            _f32p, _f32p, _f32p]
+        L.oracle_page_lookup.restype = ctypes.c_int
+        L.oracle_page_lookup.argtypes = [_i32p] + [ctypes.c_int] * 6
+        L.oracle_minmax_scale.restype = ctypes.c_float
+        L.oracle_minmax_scale.argtypes = [_f32p, ctypes.c_int64]
+        L.oracle_quantize.argtypes = [_f32p, ctypes.c_int64, ctypes.c_float, _i8p]
+        L.oracle_quantize_rows.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _i8p, _f32p]
+        L.oracle_quantize_cols.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _i8p, _f32p]
+        L.oracle_i8_gemm.argtypes = [_i8p, _i8p, _i32p, _f32p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, _f32p, _f32p, _f32p, ctypes.c_int]
+        L.oracle_layer_norm.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
+                                        ctypes.c_float, _f32p]
+        L.oracle_mlp_f32.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,
+                                     _f32p, _f32p, _f32p, _f32p]
+        L.oracle_argmax_rows.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _i32p]
+        L.oracle_half_to_float.argtypes = [_u16p, _f32p, ctypes.c_int64]
+        L.oracle_float_to_half.argtypes = [_f32p, _u16p, ctypes.c_int64]
+        L.oracle_decoder_create.restype = ctypes.c_void_p
+        L.oracle_decoder_create.argtypes = [ctypes.POINTER(OracleModel), ctypes.c_int]
+        L.oracle_decoder_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_decoder_kv_ptr.restype = _u16p
+        L.oracle_decoder_kv_ptr.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.oracle_decoder_step.restype = ctypes.c_int
+        L.oracle_decoder_step.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_float,
+                                          ctypes.c_int, ctypes.c_int, _f32p, _f32p, _i32p]
+        L.oracle_num_threads.restype = ctypes.c_int
+
+    # -- attention ---------------------------------------------------------
+    def paged_attention(self, q, k_pool, v_pool, page_table, *, T, beam_ids=None,
+                        context_lens=None, temperature=1.0, top_k=0, top_p=1.0, eos_token=-1,
+                        eos_threshold=0.0, want_probs=False):
+        q = np.ascontiguousarray(q, np.float32)
+        B, H, D = q.shape
+        num_pages, ts, D2 = k_pool.shape
+        assert D2 == D
+        k_pool = np.ascontiguousarray(k_pool, np.float32)
+        v_pool = np.ascontiguousarray(v_pool, np.float32)
+        pt = np.ascontiguousarray(page_table, np.int32)
+        num_beams, H2, max_tiles = pt.shape
+        assert H2 == H
+        out = np.zeros((B, H, D), np.float32)
+        probs = np.zeros((B, H, T), np.float32) if want_probs else None
+        scores = np.zeros((B, H, T), np.float32) if want_probs else None
+        bi = None if beam_ids is None else np.ascontiguousarray(beam_ids, np.int32)
+        cl = None if context_lens is None else np.ascontiguousarray(context_lens, np.int32)
+        rc = self.lib.oracle_paged_attention(
+            _ptr(q, _f32p), _ptr(k_pool, _f32p), _ptr(v_pool, _f32p), _ptr(pt, _i32p),
+            num_pages, ts, num_beams, max_tiles, _ptr(bi, _i32p), _ptr(cl, _i32p),
+            B, H, D, T, temperature, top_k, top_p, eos_token, eos_threshold,
+            _ptr(out, _f32p), _ptr(probs, _f32p), _ptr(scores, _f32p))
+        assert rc == 0
+        return (out, probs, scores) if want_probs else out
+
+    # -- int8 ---------------------------------------------------------------
+    def quantize_rows(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        rows, cols = x.shape
+        q = np.empty((rows, cols), np.int8)
+        s = np.empty(rows, np.float32)
+        self.lib.oracle_quantize_rows(_ptr(x, _f32p), rows, cols, _ptr(q, _i8p), _ptr(s, _f32p))
+        return q, s
+
+    def quantize_cols(self, w):
+        w = np.ascontiguousarray(w, np.float32)
+        K, N = w.shape
+        q = np.empty((K, N), np.int8)
+        s = np.empty(N, np.float32)
+        self.lib.oracle_quantize_cols(_ptr(w, _f32p), K, N, _ptr(q, _i8p), _ptr(s, _f32p))
+        return q, s
+
+    def i8_gemm(self, A, W, sa=None, sw=None, bias=None, act=0):
+        A = np.ascontiguousarray(A, np.int8)
+        W = np.ascontiguousarray(W, np.int8)
+        M, K = A.shape
+        K2, N = W.shape
+        assert K == K2
+        acc = np.empty((M, N), np.int32)
+        C = np.empty((M, N), np.float32)
+        f = lambda a: None if a is None else np.ascontiguousarray(a, np.float32)
+        sa, sw, bias = f(sa), f(sw), f(bias)
+        self.lib.oracle_i8_gemm(_ptr(A, _i8p), _ptr(W, _i8p), _ptr(acc, _i32p), _ptr(C, _f32p),
+                                M, N, K, _ptr(sa, _f32p), _ptr(sw, _f32p), _ptr(bias, _f32p), act)
+        return acc, C
+
+    def layer_norm(self, x, gamma, beta, eps=1e-5):
+        x = np.ascontiguousarray(x, np.float32)
+        rows, cols = x.shape
+        out = np.empty_like(x)
+        self.lib.oracle_layer_norm(_ptr(x, _f32p), rows, cols,
+                                   _ptr(np.ascontiguousarray(gamma, np.float32), _f32p),
+                                   _ptr(np.ascontiguousarray(beta, np.float32), _f32p), eps,
+                                   _ptr(out, _f32p))
+        return out
+
+    def mlp_f32(self, x, w1, b1, w2, b2):
+        x = np.ascontiguousarray(x, np.float32)
+        rows, hid = x.shape
+        inter = w1.shape[1]
+        out = np.empty((rows, hid), np.float32)
+        c = lambda a: np.ascontiguousarray(a, np.float32)
+        w1, b1, w2, b2 = c(w1), c(b1), c(w2), c(b2)
+        self.lib.oracle_mlp_f32(_ptr(x, _f32p), rows, hid, inter, _ptr(w1, _f32p),
+                                _ptr(b1, _f32p), _ptr(w2, _f32p), _ptr(b2, _f32p),
+                                _ptr(out, _f32p))
+        return out
+
+    def argmax_rows(self, logits):
+        logits = np.ascontiguousarray(logits, np.float32)
+        rows, V = logits.shape
+        out = np.empty(rows, np.int32)
+        self.lib.oracle_argmax_rows(_ptr(logits, _f32p), rows, V, _ptr(out, _i32p))
+        return out
+
+    def num_threads(self) -> int:
+        return int(self.lib.oracle_num_threads())
+
+
+class OracleDecoder:
+    """Restated INT8Decoder (contiguous fp16 KV) over host weights (see
+    ``synthetic_int8_model``)."""
+
+    def __init__(self, oracle: Oracle, w: dict, B: int):
+        self.o = oracle
+        self.w = w  # keep arrays alive
+        cfg = w["cfg"]
+        m = OracleModel()
+        m.L, m.H, m.D, m.hid, m.inter, m.V, m.max_seq = (
+            cfg["L"], cfg["H"], cfg["D"], cfg["hid"], cfg["inter"], cfg["V"], cfg["max_seq"])
+        m.emb = _ptr(w["emb"].view(np.uint16), _u16p)
+        for name in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "sw_qkv", "sw_o", "sw1", "b1", "sw2", "b2"):
+            setattr(m, name, _ptr(w[name], _f32p))
+        for name in ("wqkv", "wo", "w1", "w2"):
+            setattr(m, name, _ptr(w[name], _i8p))
+        self.model = m
+        self.B = B
+        self.cfg = cfg
+        self.h = oracle.lib.oracle_decoder_create(ctypes.byref(m), B)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.o.lib.oracle_decoder_destroy(self.h)
+            self.h = None
+
+    def kv(self, layer: int, which: int) -> np.ndarray:
+        """fp16 view [B][H][max_seq][D] of layer's K (which=0) or V (which=1)."""
+        c = self.cfg
+        p = self.o.lib.oracle_decoder_kv_ptr(self.h, layer, which)
+        n = self.B * c["H"] * c["max_seq"] * c["D"]
+        arr = np.ctypeslib.as_array(p, shape=(n,)).view(np.float16)
+        return arr.reshape(self.B, c["H"], c["max_seq"], c["D"])
+
+    def step(self, tokens, pos, attn_scale=1.0, layers=-1, lm_head=True):
+        c = self.cfg
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        pos = np.ascontiguousarray(pos, np.int32)
+        x = np.empty((self.B, c["hid"]), np.float32)
+        logits = np.empty((self.B, c["V"]), np.float32) if lm_head else None
+        nxt = np.empty(self.B, np.int32) if lm_head else None
+        rc = self.o.lib.oracle_decoder_step(self.h, _ptr(tokens, _i32p), _ptr(pos, _i32p),
+                                            attn_scale, layers, 1 if lm_head else 0,
+                                            _ptr(x, _f32p), _ptr(logits, _f32p),
+                                            _ptr(nxt, _i32p))
+        assert rc == 0, rc
+        return x, logits, nxt
+
+
+# ---------------------------------------------------------------------------
+# numpy helpers shared by tests / bench (host-side data preparation)
+# ---------------------------------------------------------------------------
+
+def quantize_rows_np(x: np.ndarray):
+    """numpy mirror of int8_quant.cpp per-row quantisation (round half away)."""
+    x = np.asarray(x, np.float32)
+    absmax = np.maximum(np.abs(x.min(axis=1)), np.abs(x.max(axis=1)))
+    scale = (np.float32(127.0) / (absmax + np.float32(1e-6))).astype(np.float32)
+    y = (x * scale[:, None]).astype(np.float64)  # float32 product, exact in f64
+    q = np.clip(np.sign(y) * np.floor(np.abs(y) + 0.5), -128, 127).astype(np.int8)
+    return q, (np.float32(1.0) / scale).astype(np.float32)
+
+
+def synthetic_int8_model(oracle: Oracle, *, L, H, D, V, max_seq, seed=1234, inter=None,
+                         fast=False):
+    """Seeded synthetic INT8Decoder weights: FP weights ~ N(0, 0.02),
+    per-output-column int8 quantisation with int8_quant.cpp semantics; LN
+    gamma ~ 1 + N(0, 0.1), beta ~ N(0, 0.1); biases ~ N(0, 0.02); embedding /
+    tied LM head fp16 ~ N(0, 1).  ``fast=True`` draws the int8 weights and scales
+    directly (bench-size models, same shapes, no fp32 staging)."""
+    hid = H * D
+    inter = inter or 4 * hid
+    rng = np.random.default_rng(seed)
+    w = {"cfg": dict(L=L, H=H, D=D, hid=hid, inter=inter, V=V, max_seq=max_seq)}
+    w["emb"] = rng.standard_normal((V, hid), dtype=np.float32).astype(np.float16)
+    w["ln1_g"] = (1 + 0.1 * rng.standard_normal((L, hid), dtype=np.float32)).astype(np.float32)
+    w["ln1_b"] = (0.1 * rng.standard_normal((L, hid), dtype=np.float32)).astype(np.float32)
+    w["ln2_g"] = (1 + 0.1 * rng.standard_normal((L, hid), dtype=np.float32)).astype(np.float32)
+    w["ln2_b"] = (0.1 * rng.standard_normal((L, hid), dtype=np.float32)).astype(np.float32)
+    shapes = {"wqkv": (hid, 3 * hid), "wo": (hid, hid), "w1": (hid, inter), "w2": (inter, hid)}
+    scales = {"wqkv": "sw_qkv", "wo": "sw_o", "w1": "sw1", "w2": "sw2"}
+    for name, (K, N) in shapes.items():
+        qs = np.empty((L, K, N), np.int8)
+        ss = np.empty((L, N), np.float32)
+        for l in range(L):
+            if fast:
+                qs[l] = rng.integers(-127, 128, size=(K, N), dtype=np.int8)
+                ss[l] = np.float32(0.02 * 3.5 / 127.0)
+            else:
+                wf = (0.02 * rng.standard_normal((K, N), dtype=np.float32)).astype(np.float32)
+                qs[l], ss[l] = oracle.quantize_cols(wf)
+        w[name] = qs
+        w[scales[name]] = ss
+    w["b1"] = (0.02 * rng.standard_normal((L, inter), dtype=np.float32)).astype(np.float32)
+    w["b2"] = (0.02 * rng.standard_normal((L, hid), dtype=np.float32)).astype(np.float32)
+    return w
+
+
+def shuffled_page_table(rng, num_beams, H, max_tiles, ntiles, num_pages=None, missing=()):
+    """Page table [num_beams][H][max_tiles] filled for the first ntiles tiles with a
+    shuffled permutation of the page pool (non-contiguous gather);
+    entries listed in ``missing`` (beam, head, tile) are -1."""
+    need = num_beams * H * ntiles
+    num_pages = num_pages or need
+    perm = rng.permutation(num_pages)[:need].astype(np.int32)
+    pt = np.full((num_beams, H, max_tiles), -1, np.int32)
+    pt[:, :, :ntiles] = perm.reshape(num_beams, H, ntiles)
+    for (b, h, t) in missing:
+        pt[b, h, t] = -1
+    return pt
