@@ -1,0 +1,257 @@
+/*
+ * llm_decoder.h — C ABI of the MI355X (gfx950) paged-attention decode path.
+ *
+ * This is the drop-in boundary: plain pointers, sizes and opaque handles, no
+ * torch or HIP types (a hipStream_t is passed as `void*`).  Every entry point
+ * returns 0 (LLM_OK) or one of the llm_status codes; llm_last_error() gives a
+ * message for the calling thread.  The pybind11 module `llm_decoder`
+ * (csrc/bindings.cpp) wraps these exactly as the reference's
+ * src/bindings.cpp:3-35 exposes its classes, mapping non-zero status to
+ * RuntimeError (the reference's loaders throw std::runtime_error,
+ * decoder/decoder_block.hpp:13-19).
+ *
+ * Citations are file:line in the reference tree.
+ */
+#ifndef LLM_DECODER_H_
+#define LLM_DECODER_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum llm_status {
+  LLM_OK = 0,
+  LLM_ERR_INVALID = 1,      /* bad shape / argument (checked on the host before any launch) */
+  LLM_ERR_UNSUPPORTED = 2,  /* valid request this build does not implement (e.g. top-k in attention) */
+  LLM_ERR_HIP = 3,          /* HIP runtime error */
+  LLM_ERR_OOM = 4,          /* device or page-pool allocation failure */
+  LLM_ERR_IO = 5            /* weight / cache file I/O */
+};
+
+enum llm_dtype { LLM_F16 = 0, LLM_I8 = 1, LLM_F32 = 2 };
+enum llm_act { LLM_ACT_NONE = 0, LLM_ACT_RELU = 1, LLM_ACT_GELU = 2 };
+
+const char* llm_last_error(void);
+int llm_abi_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Paged decode attention                                                    */
+/* ------------------------------------------------------------------------ */
+
+/* POD device view of one layer's KV pools + page table, passed BY VALUE to the
+ * kernel.  Replaces handing the host KVTileCache object (std containers,
+ * mutex) to device code (attention/attention_tile_launcher.hpp:43,
+ * attention/paged_flash_attention_kernel_fused.cu:13).  Semantics of
+ * KVTileCache<T>::get (kv_cache/kv_tile_cache.hpp:21-26) and
+ * PageTable::lookup (kv_cache/page_table.hpp:39-49): entry
+ * page_table[(beam*num_heads + head)*max_tiles + tile]; a page < 0 or
+ * >= num_pages means "no tile" (its tokens are masked). */
+typedef struct pa_kv_view {
+  const void* k_pool;         /* [num_pages][page_size][head_dim] fp16 */
+  const void* v_pool;         /* same layout */
+  const int32_t* page_table;  /* [num_beams][num_heads][max_tiles] int32, device */
+  int32_t num_pages;
+  int32_t page_size;          /* tokens per page (tile_size) */
+  int32_t head_dim;
+  int32_t num_beams;
+  int32_t num_heads;
+  int32_t max_tiles;
+  int32_t kv_dtype;           /* LLM_F16 */
+} pa_kv_view;
+
+/* Bytes of device workspace pa_decode needs (split-T partial softmax state). */
+size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles, int pages_per_split);
+
+/* Split-T count heuristic used when pages_per_split <= 0: enough waves to
+ * fill 256 CUs.  Returns the pages-per-split pa_decode will use. */
+int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles);
+
+/* Paged decode attention (replaces paged_flash_attention_kernel_fused,
+ * attention/paged_flash_attention_kernel_fused.cu:5-90, launched by
+ * AttentionTileLauncher::launch, attention/attention_tile_launcher.hpp:36-89,
+ * from AttentionCUDA::forward, attention/attention_cuda.cu:41-95), with the
+ * INTENDED maths of cpu_paged_attention_forward
+ * (attention_cpu/cpu_attention_kernel.cpp:37-129):
+ *   r = beam_ids ? beam_ids[b] : b;  T_b = context_lens ? context_lens[b] : T
+ *   s_t = (q[b,h] . k_t) * sm_scale        (sm_scale = 1/temperature^2 reproduces
+ *                                           the reference's double division)
+ *   out[b,h] = sum_t exp(s_t - max s) v_t / (sum_t exp(s_t - max s) + 1e-6)
+ * over t < T_b whose page is present.  q, out: fp32 [B][H][D] device.
+ * pages_per_split <= 0 selects pa_decode_pages_per_split().  workspace may be
+ * NULL when the call needs none (single split). */
+int pa_decode(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
+              const int32_t* context_lens, int B, int H, int D, int T, float sm_scale,
+              int pages_per_split, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* INT8 / FP16 weight GEMMs (MFMA)                                          */
+/* ------------------------------------------------------------------------ */
+
+/* Bytes of the packed (MFMA-fragment-ordered) weight for a [K][N] matrix. */
+size_t gemm_packed_bytes(int dtype, int K, int N);
+
+/* Repack W [K][N] row-major (the reference layout, decoder/mlp.hpp:28-31) into
+ * the MFMA fragment order the GEMM streams (device -> device). */
+int gemm_pack_weights(int dtype, const void* W_kn, void* W_packed, int K, int N, void* stream);
+
+/* INT8 GEMM, contract of dnnl_matmul_int8 (attention_cpu/dnnl_matmul_int8.cpp:7-75)
+ * restated for decode:
+ *   acc[m,n] = sum_k int32(A[m,k]) * int32(W[k,n])          exact int32
+ *   C[m,n]   = act(float(acc) * (sa[m] * sw[n]) + bias[n])  fp32
+ * A int8 [M][K] (row stride lda >= K), W_packed from gemm_pack_weights.
+ * sa / sw / bias may be NULL (1, 1, 0).  acc_out (int32 [M][N]) and C
+ * (fp32 [M][N]) may each be NULL.  K % 64 == 0, N % 16 == 0. */
+int i8_gemm(const int8_t* A, int lda, const void* W_packed, int32_t* acc_out, float* C,
+            int M, int N, int K, const float* sa, const float* sw, const float* bias,
+            int act, void* stream);
+
+/* FP16 GEMM with fp32 accumulate (CUDADecoder weights):
+ *   C[m,n] = act(sum_k A[m,k] W[k,n] + bias[n]),  A fp16 [M][K], K % 32 == 0. */
+int f16_gemm(const void* A, int lda, const void* W_packed, float* C, int M, int N, int K,
+             const float* bias, int act, void* stream);
+
+/* Tied-embedding LM head: logits[m,v] = sum_k x[m,k] * E[v,k], x fp32 [M][K],
+ * E fp16 [V][K] (token_embedding.hpp layout).  x is split hi+lo into two fp16
+ * MFMA operands so the product keeps ~fp32 accuracy.  K % 32 == 0. */
+int lm_head(const float* x, const void* E, float* logits, int M, int V, int K, void* stream);
+
+/* Row-wise argmax (first maximum wins, std::max_element, decoder/cuda_decoder.cu:7-14). */
+int argmax_rows(const float* logits, int rows, int V, int32_t* out, void* stream);
+
+/* Per-row dynamic int8 quantisation (attention_cpu/int8_quant.cpp:5-13,59-64):
+ * scale_r = 127/(absmax_r + 1e-6); q = clamp(round(x*scale_r)); inv_scale[r] = 1/scale_r. */
+int quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv_scale, void* stream);
+
+/* LayerNorm (decoder/layer_norm.hpp:20-37) fused with per-row int8 quantisation
+ * (q/inv_scale may be NULL: then only `out` fp32 is written; out may be NULL). */
+int layernorm_quant(const float* x, int rows, int cols, const float* gamma, const float* beta,
+                    float eps, float* out, int8_t* q, float* inv_scale, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* KV cache: page pools + page table (kv_cache/page_table.hpp:5-37,          */
+/* kv_cache/kv_tile_cache.hpp:9-80) with a layer dimension, a free-list page */
+/* allocator (replacing the map.size() ids of kv_tile_cache.cpp:71) and a    */
+/* single host source of truth synchronised to the device.                   */
+/* ------------------------------------------------------------------------ */
+typedef struct kv_cache kv_cache;
+
+int kv_cache_create(int num_layers, int num_beams, int num_heads, int head_dim, int page_size,
+                    int max_tiles, long long num_pages, kv_cache** out);
+void kv_cache_destroy(kv_cache* c);
+int kv_cache_view(const kv_cache* c, int layer, pa_kv_view* out);
+long long kv_cache_num_pages(const kv_cache* c);
+long long kv_cache_free_pages(const kv_cache* c);
+/* PageTable::assign (page_table.cpp:49-53) / lookup / remove (:64-66), host mirror. */
+int kv_cache_assign(kv_cache* c, int layer, int beam, int head, int tile, int page);
+int kv_cache_lookup(const kv_cache* c, int layer, int beam, int head, int tile);
+int kv_cache_remove(kv_cache* c, int layer, int beam, int head, int tile);
+/* KVTileCache::register_tile (kv_tile_cache.cpp:64-77): allocate a free page
+ * for (layer, beam, head, tile) if it has none; returns the page id in *page. */
+int kv_cache_register_tile(kv_cache* c, int layer, int beam, int head, int tile, int* page);
+/* Ensure pages exist for tiles covering tokens [0, n_tokens) of `beam`, all layers/heads. */
+int kv_cache_reserve(kv_cache* c, int beam, int n_tokens);
+/* Beam fork: dst's page-table rows := src's (all layers, heads), shared pages
+ * refcounted; pages of dst are copied-on-write by kv_cache_append/write. */
+int kv_cache_fork(kv_cache* c, int src_beam, int dst_beam);
+/* Release every page of `beam` (refcount-aware). */
+int kv_cache_release(kv_cache* c, int beam);
+/* PageTable::clear (page_table.cpp:39-44): all entries -1, all pages free. */
+int kv_cache_clear(kv_cache* c);
+/* PageTable::sync_to_gpu (page_table.cpp:59-62): push dirty host entries. */
+int kv_cache_sync(kv_cache* c, void* stream);
+/* Copy n tokens of fp16 K and V (host, [n][H][D]) for `beam` starting at token
+ * position pos into the pools of `layer` (pages must be reserved). */
+int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, int n, const void* k_host,
+                          const void* v_host);
+/* Device pointers of the pools / table (for tests and custom kernels). */
+void* kv_cache_k_pool(kv_cache* c);
+void* kv_cache_v_pool(kv_cache* c);
+int32_t* kv_cache_page_table(kv_cache* c, int layer);
+/* KVTileCache::save_to_file / load_from_file (kv_tile_cache.cpp:105-125):
+ * header + page table + used pages. */
+int kv_cache_save(const kv_cache* c, const char* path);
+int kv_cache_load(kv_cache* c, const char* path);
+
+/* ------------------------------------------------------------------------ */
+/* Decoder (CUDADecoder / INT8Decoder, decoder/cuda_decoder.hpp:7-21,        */
+/* decoder/int8_decoder.hpp:6-17)                                            */
+/* ------------------------------------------------------------------------ */
+typedef struct llm_decoder llm_decoder;
+
+typedef struct llm_decoder_config {
+  int num_layers, num_heads, head_dim, hidden_dim, vocab_size, max_seq_len; /* ctor args, bindings.cpp:6 */
+  int inter_dim;        /* 0 -> 4*hidden_dim (decoder_block.hpp:28) */
+  int page_size;        /* 0 -> 16 */
+  int weight_dtype;     /* LLM_I8 (INT8Decoder) or LLM_F16 (CUDADecoder) */
+  int max_batch;        /* rows decoded together (0 -> 1) */
+  float attn_scale;     /* score multiplier; 1.0 = reference (no 1/sqrt(D)) */
+  long long num_pages;  /* KV page-pool size; 0 -> enough for max_batch * max_seq_len */
+} llm_decoder_config;
+
+int llm_decoder_create(const llm_decoder_config* cfg, llm_decoder** out);
+void llm_decoder_destroy(llm_decoder* d);
+
+/* Host weights (row-major reference layouts), uploaded and packed on device.
+ * INT8: wqkv [L][hid][3hid] (q|k|v, heads contiguous), wo [L][hid][hid],
+ * w1 [L][hid][inter], w2 [L][inter][hid] int8 + per-output-column fp32 dequant
+ * scales; biases b1 [L][inter], b2 [L][hid]; LayerNorm gamma/beta [L][hid];
+ * emb fp16 [V][hid] (embedding and tied LM head). */
+typedef struct llm_int8_weights {
+  const uint16_t* emb;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  const int8_t* wqkv; const float* sw_qkv;
+  const int8_t* wo;   const float* sw_o;
+  const int8_t* w1;   const float* sw1; const float* b1;
+  const int8_t* w2;   const float* sw2; const float* b2;
+} llm_int8_weights;
+int llm_decoder_set_int8_weights(llm_decoder* d, const llm_int8_weights* w);
+
+typedef struct llm_f16_weights {
+  const uint16_t* emb;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  const uint16_t *wqkv, *wo, *w1, *w2;   /* fp16, same [K][N] layouts */
+  const float *b1, *b2;
+} llm_f16_weights;
+int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights* w);
+
+/* CUDADecoder::load_weights (decoder/cuda_decoder.cu:35-45) / INT8Decoder::
+ * load_quantized_weights (decoder/int8_decoder.cpp:91-95) / quantize_weights
+ * (:43-89) over the raw little-endian .bin layout of weights/README.md:26-38. */
+int llm_decoder_load_weights(llm_decoder* d, const char* dir);
+int llm_decoder_load_quantized_weights(llm_decoder* d, const char* dir);
+int llm_quantize_weights(const char* fp32_dir, const char* int8_dir, int num_layers,
+                         int hidden_dim, int inter_dim, int vocab_size);
+
+/* Batched generate (CUDADecoder<T>::generate, decoder/cuda_decoder.cu:48-61,
+ * batched): for each row, prompt tokens are consumed one per step (KV is
+ * appended), then max_gen_len tokens are produced by greedy argmax.  out
+ * [batch][max_gen_len] receives the generated ids (prompt excluded). */
+int llm_decoder_generate(llm_decoder* d, const int32_t* prompts, const int32_t* prompt_lens,
+                         int prompt_stride, int batch, int max_gen_len, float temperature,
+                         int32_t* out);
+
+/* Low-level stepping (bench / multi-GPU driver). */
+/* Start `batch` rows whose first context_len tokens are synthetic: every page
+ * is allocated (shuffled order when shuffle != 0) and filled with seeded
+ * random fp16 K/V on device. */
+int llm_decoder_begin_synthetic(llm_decoder* d, int batch, int context_len, uint64_t seed,
+                                int shuffle);
+/* One decode step for all active rows: tokens (host [batch], or NULL to feed
+ * back the previous argmax) at each row's next position; writes fp32 logits
+ * to logits_dev ([batch][V] device, may be NULL) and copies next ids to
+ * next_host (may be NULL; a NULL next_host keeps the step asynchronous).
+ * stream NULL -> the decoder's own stream. */
+int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
+                     int32_t* next_host, void* stream);
+int llm_decoder_sync(llm_decoder* d);
+int llm_decoder_context_len(const llm_decoder* d, int row);
+kv_cache* llm_decoder_kv(llm_decoder* d);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LLM_DECODER_H_ */

@@ -1,0 +1,83 @@
+// Shared host/device helpers for the gfx950 decode path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "llm_decoder.h"
+
+namespace llm {
+
+// Thread-local last-error message (llm_last_error()).
+void set_error(const std::string& msg);
+int fail(int status, const std::string& msg);
+
+#define LLM_HIP_RET(expr)                                                        \
+  do {                                                                           \
+    hipError_t _e = (expr);                                                      \
+    if (_e != hipSuccess)                                                        \
+      return ::llm::fail(LLM_ERR_HIP, std::string(#expr " failed: ") +           \
+                                          hipGetErrorString(_e));                \
+  } while (0)
+
+#define LLM_REQUIRE(cond, msg)                                                   \
+  do {                                                                           \
+    if (!(cond)) return ::llm::fail(LLM_ERR_INVALID, msg);                       \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr float kNegSentinel = -1.0e30f;  // "minus infinity" that stays finite
+constexpr float kLog2e = 1.4426950408889634f;
+
+// DPP lane moves (row = 16 lanes).  ctrl must be a compile-time constant.
+template <int CTRL>
+__device__ __forceinline__ float mov_dpp(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over aligned groups of G lanes (G in {2,4,8,16,32,64}); every lane of a
+// group ends with the identical total (commutative butterfly).
+template <int G>
+__device__ __forceinline__ float group_sum(float x) {
+  if constexpr (G >= 2) x += mov_dpp<0xB1>(x);   // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) x += mov_dpp<0x4E>(x);   // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) x += mov_dpp<0x141>(x);  // row_half_mirror
+  if constexpr (G >= 16) x += mov_dpp<0x140>(x); // row_mirror
+  if constexpr (G >= 32) x += __shfl_xor(x, 16, 64);
+  if constexpr (G >= 64) x += __shfl_xor(x, 32, 64);
+  return x;
+}
+
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x = fmaxf(x, __shfl_xor(x, off, 64));
+  return x;
+}
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+__device__ __forceinline__ int wave_id_uniform() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+}  // namespace llm

@@ -1,0 +1,488 @@
+// KV page pools + page table (host runtime), compiled as HIP.
+//
+// Replaces PageTable (kv_cache/page_table.{hpp,cpp}) and KVTileCache<T>
+// (kv_cache/kv_tile_cache.{hpp,cpp}) with:
+//   * a layer dimension: table [L][beams][H][max_tiles] (the reference shares
+//     one table across layers, Appendix A #11, and sizes it (pages, D, ts),
+//     kv_tile_cache.cpp:23 — both defects);
+//   * ONE source of truth: the host mirror; the device table is updated by
+//     kv_cache_sync() with a scatter of the dirty entries (the reference's
+//     assign() writes only the device, remove() only the host, and
+//     sync_to_gpu() overwrites the device, page_table.cpp:49-66);
+//   * a free-list page allocator with per-page refcounts (the reference's
+//     page id = map.size() aliases live pages after an eviction,
+//     kv_tile_cache.cpp:71), so beams can fork and share prefix pages;
+//   * copy-on-write of a shared page before a token is written into it.
+// Pools are one hipMalloc each ([num_pages][page_size][head_dim] fp16), sized
+// for the 288 GB HBM of an MI355X (page ids are int32, byte offsets 64-bit).
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kv_cache_impl.hpp"
+#include "row_ops.hpp"
+
+namespace llm {
+
+// src [n][H][D] fp16 rows for token positions pos0..pos0+n-1 of `beam`.
+__global__ void kv_write_tokens_kernel(const _Float16* __restrict__ ksrc,
+                                       const _Float16* __restrict__ vsrc, int n, int H, int D,
+                                       int pos0, int beam, const int32_t* __restrict__ table,
+                                       int max_tiles, int TS, long long num_pages,
+                                       _Float16* __restrict__ kp, _Float16* __restrict__ vp) {
+  const size_t total = (size_t)n * H * D;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int d = i % D;
+    const int h = (i / D) % H;
+    const int t = i / ((size_t)H * D);
+    const int pos = pos0 + t;
+    const int tile = pos / TS;
+    if (tile >= max_tiles) continue;
+    const int page = table[((size_t)beam * H + h) * max_tiles + tile];
+    if (page < 0 || page >= num_pages) continue;
+    const size_t off = ((size_t)page * TS + pos % TS) * D + d;
+    kp[off] = ksrc[i];
+    vp[off] = vsrc[i];
+  }
+}
+
+int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, long long pages) {
+  L = L_; beams = beams_; H = H_; D = D_; TS = TS_; max_tiles = max_tiles_; num_pages = pages;
+  page_elems = (size_t)TS * D;
+  const size_t pool_bytes = (size_t)num_pages * page_elems * 2;
+  if (hipMalloc(&k_pool, pool_bytes) != hipSuccess || hipMalloc(&v_pool, pool_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(LLM_ERR_OOM, "kv_cache: cannot allocate " + std::to_string(2 * pool_bytes) +
+                                 " bytes of page pool");
+  }
+  entries = (size_t)L * beams * H * max_tiles;
+  LLM_HIP_RET(hipMalloc(&d_table, entries * sizeof(int32_t)));
+  LLM_HIP_RET(hipMemset(d_table, 0xFF, entries * sizeof(int32_t)));  // -1 (page_table.cpp:22-25)
+  h_table.assign(entries, -1);
+  dirty_flag.assign(entries, 0);
+  refcount.assign((size_t)num_pages, 0);
+  free_list.resize((size_t)num_pages);
+  for (long long i = 0; i < num_pages; ++i) free_list[i] = (int32_t)(num_pages - 1 - i);
+  LLM_HIP_RET(hipEventCreateWithFlags(&staging_done, hipEventDisableTiming));
+  return LLM_OK;
+}
+
+KvCache::~KvCache() {
+  if (staging_done) (void)hipEventSynchronize(staging_done);
+  if (k_pool) (void)hipFree(k_pool);
+  if (v_pool) (void)hipFree(v_pool);
+  if (d_table) (void)hipFree(d_table);
+  if (d_idx) (void)hipFree(d_idx);
+  if (d_val) (void)hipFree(d_val);
+  if (h_idx) (void)hipHostFree(h_idx);
+  if (h_val) (void)hipHostFree(h_val);
+  if (staging_done) (void)hipEventDestroy(staging_done);
+}
+
+bool KvCache::in_range(int layer, int beam, int head, int tile) const {
+  return layer >= 0 && layer < L && beam >= 0 && beam < beams && head >= 0 && head < H &&
+         tile >= 0 && tile < max_tiles;
+}
+
+void KvCache::set_entry(size_t idx, int32_t page) {
+  h_table[idx] = page;
+  if (!dirty_flag[idx]) {
+    dirty_flag[idx] = 1;
+    dirty.push_back((int64_t)idx);
+  }
+}
+
+int KvCache::alloc_page(int32_t* out) {
+  if (free_list.empty())
+    return fail(LLM_ERR_OOM, "kv_cache: page pool exhausted (" + std::to_string(num_pages) +
+                                 " pages)");
+  *out = free_list.back();
+  free_list.pop_back();
+  refcount[*out] = 1;
+  return LLM_OK;
+}
+
+void KvCache::drop_page(int32_t page) {
+  if (page < 0 || page >= num_pages) return;
+  if (--refcount[page] <= 0) {
+    refcount[page] = 0;
+    free_list.push_back(page);
+  }
+}
+
+int KvCache::ensure_tile(int layer, int beam, int head, int tile, bool exclusive, int32_t* page) {
+  const size_t idx = index(layer, beam, head, tile);
+  int32_t p = h_table[idx];
+  if (p < 0) {
+    int rc = alloc_page(&p);
+    if (rc) return rc;
+    set_entry(idx, p);
+  } else if (exclusive && refcount[p] > 1) {
+    // copy-on-write: the page is shared with a forked beam
+    int32_t np;
+    int rc = alloc_page(&np);
+    if (rc) return rc;
+    cow.push_back({p, np});
+    refcount[p] -= 1;
+    set_entry(idx, np);
+    p = np;
+  }
+  if (page) *page = p;
+  return LLM_OK;
+}
+
+int KvCache::prepare_append(int beam, int pos) {
+  const int tile = pos / TS;
+  if (tile >= max_tiles)
+    return fail(LLM_ERR_INVALID, "kv_cache: position " + std::to_string(pos) +
+                                     " beyond max_tiles*page_size");
+  for (int l = 0; l < L; ++l)
+    for (int h = 0; h < H; ++h) {
+      int rc = ensure_tile(l, beam, h, tile, true, nullptr);
+      if (rc) return rc;
+    }
+  return LLM_OK;
+}
+
+int KvCache::sync(hipStream_t st) {
+  // pending copy-on-write page copies first (old page -> new page, K and V)
+  for (const auto& c : cow) {
+    const size_t bytes = page_elems * 2;
+    LLM_HIP_RET(hipMemcpyAsync((char*)k_pool + (size_t)c.second * bytes,
+                               (char*)k_pool + (size_t)c.first * bytes, bytes,
+                               hipMemcpyDeviceToDevice, st));
+    LLM_HIP_RET(hipMemcpyAsync((char*)v_pool + (size_t)c.second * bytes,
+                               (char*)v_pool + (size_t)c.first * bytes, bytes,
+                               hipMemcpyDeviceToDevice, st));
+  }
+  cow.clear();
+  if (dirty.empty()) return LLM_OK;
+  const size_t n = dirty.size();
+  if (n * 4 > entries) {  // mostly dirty: push the whole table
+    LLM_HIP_RET(hipEventSynchronize(staging_done));
+    LLM_HIP_RET(hipMemcpyAsync(d_table, h_table.data(), entries * sizeof(int32_t),
+                               hipMemcpyHostToDevice, st));
+    LLM_HIP_RET(hipStreamSynchronize(st));  // pageable source: keep it valid until copied
+  } else {
+    LLM_HIP_RET(hipEventSynchronize(staging_done));  // previous staging consumed
+    if (n > staging_cap) {
+      if (d_idx) LLM_HIP_RET(hipFree(d_idx));
+      if (d_val) LLM_HIP_RET(hipFree(d_val));
+      if (h_idx) LLM_HIP_RET(hipHostFree(h_idx));
+      if (h_val) LLM_HIP_RET(hipHostFree(h_val));
+      staging_cap = std::max<size_t>(n, 4096);
+      LLM_HIP_RET(hipMalloc(&d_idx, staging_cap * sizeof(int64_t)));
+      LLM_HIP_RET(hipMalloc(&d_val, staging_cap * sizeof(int32_t)));
+      LLM_HIP_RET(hipHostMalloc(&h_idx, staging_cap * sizeof(int64_t), hipHostMallocDefault));
+      LLM_HIP_RET(hipHostMalloc(&h_val, staging_cap * sizeof(int32_t), hipHostMallocDefault));
+    }
+    for (size_t i = 0; i < n; ++i) {
+      h_idx[i] = dirty[i];
+      h_val[i] = h_table[dirty[i]];
+    }
+    LLM_HIP_RET(hipMemcpyAsync(d_idx, h_idx, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    LLM_HIP_RET(hipMemcpyAsync(d_val, h_val, n * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    LLM_HIP_RET(launch_scatter_i32(d_table, d_idx, d_val, (int)n, st));
+    LLM_HIP_RET(hipEventRecord(staging_done, st));
+  }
+  for (int64_t i : dirty) dirty_flag[i] = 0;
+  dirty.clear();
+  return LLM_OK;
+}
+
+}  // namespace llm
+
+using namespace llm;
+
+struct kv_cache {
+  KvCache impl;
+};
+
+extern "C" int kv_cache_create(int num_layers, int num_beams, int num_heads, int head_dim,
+                               int page_size, int max_tiles, long long num_pages, kv_cache** out) {
+  LLM_REQUIRE(out != nullptr, "kv_cache_create: out is NULL");
+  LLM_REQUIRE(num_layers > 0 && num_beams > 0 && num_heads > 0 && head_dim > 0 && page_size > 0 &&
+                  max_tiles > 0 && num_pages > 0,
+              "kv_cache_create: all sizes must be positive");
+  LLM_REQUIRE(num_pages < (1LL << 31), "kv_cache_create: num_pages must fit int32");
+  auto* c = new kv_cache();
+  int rc = c->impl.init(num_layers, num_beams, num_heads, head_dim, page_size, max_tiles, num_pages);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return LLM_OK;
+}
+
+extern "C" void kv_cache_destroy(kv_cache* c) { delete c; }
+
+KvCache* kv_impl(kv_cache* c) { return c ? &c->impl : nullptr; }
+
+extern "C" int kv_cache_view(const kv_cache* c, int layer, pa_kv_view* out) {
+  LLM_REQUIRE(c && out, "kv_cache_view: NULL");
+  const KvCache& k = c->impl;
+  LLM_REQUIRE(layer >= 0 && layer < k.L, "kv_cache_view: bad layer");
+  out->k_pool = k.k_pool;
+  out->v_pool = k.v_pool;
+  out->page_table = k.d_table + (size_t)layer * k.beams * k.H * k.max_tiles;
+  out->num_pages = (int32_t)k.num_pages;
+  out->page_size = k.TS;
+  out->head_dim = k.D;
+  out->num_beams = k.beams;
+  out->num_heads = k.H;
+  out->max_tiles = k.max_tiles;
+  out->kv_dtype = LLM_F16;
+  return LLM_OK;
+}
+
+extern "C" long long kv_cache_num_pages(const kv_cache* c) { return c ? c->impl.num_pages : -1; }
+
+extern "C" long long kv_cache_free_pages(const kv_cache* c) {
+  if (!c) return -1;
+  std::lock_guard<std::mutex> g(const_cast<kv_cache*>(c)->impl.mu);
+  return (long long)c->impl.free_list.size();
+}
+
+extern "C" int kv_cache_assign(kv_cache* c, int layer, int beam, int head, int tile, int page) {
+  LLM_REQUIRE(c, "kv_cache_assign: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_REQUIRE(k.in_range(layer, beam, head, tile), "kv_cache_assign: index out of range");
+  LLM_REQUIRE(page >= -1 && page < k.num_pages, "kv_cache_assign: page out of range");
+  const size_t idx = k.index(layer, beam, head, tile);
+  const int32_t old = k.h_table[idx];
+  if (old == page) return LLM_OK;
+  if (page >= 0) {
+    // take the page out of the free list if it is there; bump its refcount
+    auto it = std::find(k.free_list.begin(), k.free_list.end(), page);
+    if (it != k.free_list.end()) k.free_list.erase(it);
+    k.refcount[page] += 1;
+  }
+  k.drop_page(old);
+  k.set_entry(idx, page);
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_lookup(const kv_cache* c, int layer, int beam, int head, int tile) {
+  if (!c) return -1;
+  const KvCache& k = c->impl;
+  if (!k.in_range(layer, beam, head, tile)) return -1;  // page_table.hpp:47
+  return k.h_table[k.index(layer, beam, head, tile)];
+}
+
+extern "C" int kv_cache_remove(kv_cache* c, int layer, int beam, int head, int tile) {
+  return kv_cache_assign(c, layer, beam, head, tile, -1);
+}
+
+extern "C" int kv_cache_register_tile(kv_cache* c, int layer, int beam, int head, int tile,
+                                      int* page) {
+  LLM_REQUIRE(c, "kv_cache_register_tile: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_REQUIRE(k.in_range(layer, beam, head, tile), "kv_cache_register_tile: index out of range");
+  int32_t p;
+  int rc = k.ensure_tile(layer, beam, head, tile, false, &p);
+  if (rc) return rc;
+  if (page) *page = p;
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_reserve(kv_cache* c, int beam, int n_tokens) {
+  LLM_REQUIRE(c, "kv_cache_reserve: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_REQUIRE(beam >= 0 && beam < k.beams && n_tokens >= 0, "kv_cache_reserve: bad beam/n");
+  const int nt = (n_tokens + k.TS - 1) / k.TS;
+  LLM_REQUIRE(nt <= k.max_tiles, "kv_cache_reserve: n_tokens exceeds max_tiles*page_size");
+  for (int l = 0; l < k.L; ++l)
+    for (int h = 0; h < k.H; ++h)
+      for (int t = 0; t < nt; ++t) {
+        int rc = k.ensure_tile(l, beam, h, t, false, nullptr);
+        if (rc) return rc;
+      }
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_fork(kv_cache* c, int src_beam, int dst_beam) {
+  LLM_REQUIRE(c, "kv_cache_fork: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_REQUIRE(src_beam >= 0 && src_beam < k.beams && dst_beam >= 0 && dst_beam < k.beams,
+              "kv_cache_fork: bad beam");
+  if (src_beam == dst_beam) return LLM_OK;
+  for (int l = 0; l < k.L; ++l)
+    for (int h = 0; h < k.H; ++h)
+      for (int t = 0; t < k.max_tiles; ++t) {
+        const size_t si = k.index(l, src_beam, h, t), di = k.index(l, dst_beam, h, t);
+        const int32_t sp = k.h_table[si], dp = k.h_table[di];
+        if (sp == dp) continue;
+        if (sp >= 0) k.refcount[sp] += 1;
+        k.drop_page(dp);
+        k.set_entry(di, sp);
+      }
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_release(kv_cache* c, int beam) {
+  LLM_REQUIRE(c, "kv_cache_release: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_REQUIRE(beam >= 0 && beam < k.beams, "kv_cache_release: bad beam");
+  for (int l = 0; l < k.L; ++l)
+    for (int h = 0; h < k.H; ++h)
+      for (int t = 0; t < k.max_tiles; ++t) {
+        const size_t i = k.index(l, beam, h, t);
+        if (k.h_table[i] >= 0) {
+          k.drop_page(k.h_table[i]);
+          k.set_entry(i, -1);
+        }
+      }
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_clear(kv_cache* c) {
+  LLM_REQUIRE(c, "kv_cache_clear: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_HIP_RET(hipEventSynchronize(k.staging_done));
+  std::fill(k.h_table.begin(), k.h_table.end(), -1);
+  std::fill(k.dirty_flag.begin(), k.dirty_flag.end(), 0);
+  k.dirty.clear();
+  k.cow.clear();
+  std::fill(k.refcount.begin(), k.refcount.end(), 0);
+  k.free_list.resize((size_t)k.num_pages);
+  for (long long i = 0; i < k.num_pages; ++i) k.free_list[i] = (int32_t)(k.num_pages - 1 - i);
+  LLM_HIP_RET(hipMemset(k.d_table, 0xFF, k.entries * sizeof(int32_t)));
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_sync(kv_cache* c, void* stream) {
+  LLM_REQUIRE(c, "kv_cache_sync: NULL");
+  std::lock_guard<std::mutex> g(c->impl.mu);
+  return c->impl.sync(as_stream(stream));
+}
+
+extern "C" int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, int n,
+                                     const void* k_host, const void* v_host) {
+  LLM_REQUIRE(c && k_host && v_host, "kv_cache_write_tokens: NULL");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  LLM_REQUIRE(layer >= 0 && layer < k.L && beam >= 0 && beam < k.beams && pos >= 0 && n >= 0,
+              "kv_cache_write_tokens: bad arguments");
+  if (n == 0) return LLM_OK;
+  LLM_REQUIRE((pos + n + k.TS - 1) / k.TS <= k.max_tiles,
+              "kv_cache_write_tokens: tokens beyond max_tiles*page_size");
+  // every target tile must exist and be exclusively owned (copy-on-write)
+  for (int t = pos / k.TS; t <= (pos + n - 1) / k.TS; ++t)
+    for (int h = 0; h < k.H; ++h) {
+      int rc = k.ensure_tile(layer, beam, h, t, true, nullptr);
+      if (rc) return rc;
+    }
+  int rc = k.sync(nullptr);
+  if (rc) return rc;
+  const size_t bytes = (size_t)n * k.H * k.D * 2;
+  void *dk = nullptr, *dv = nullptr;
+  LLM_HIP_RET(hipMalloc(&dk, bytes));
+  LLM_HIP_RET(hipMalloc(&dv, bytes));
+  LLM_HIP_RET(hipMemcpy(dk, k_host, bytes, hipMemcpyHostToDevice));
+  LLM_HIP_RET(hipMemcpy(dv, v_host, bytes, hipMemcpyHostToDevice));
+  const size_t total = (size_t)n * k.H * k.D;
+  hipLaunchKernelGGL(kv_write_tokens_kernel, dim3((unsigned)std::min<size_t>((total + 255) / 256, 65536)),
+                     dim3(256), 0, nullptr, static_cast<const _Float16*>(dk),
+                     static_cast<const _Float16*>(dv), n, k.H, k.D, pos, beam,
+                     k.d_table + (size_t)layer * k.beams * k.H * k.max_tiles, k.max_tiles, k.TS,
+                     k.num_pages, static_cast<_Float16*>(k.k_pool), static_cast<_Float16*>(k.v_pool));
+  LLM_HIP_RET(hipGetLastError());
+  LLM_HIP_RET(hipDeviceSynchronize());
+  LLM_HIP_RET(hipFree(dk));
+  LLM_HIP_RET(hipFree(dv));
+  return LLM_OK;
+}
+
+extern "C" void* kv_cache_k_pool(kv_cache* c) { return c ? c->impl.k_pool : nullptr; }
+extern "C" void* kv_cache_v_pool(kv_cache* c) { return c ? c->impl.v_pool : nullptr; }
+extern "C" int32_t* kv_cache_page_table(kv_cache* c, int layer) {
+  if (!c || layer < 0 || layer >= c->impl.L) return nullptr;
+  const KvCache& k = c->impl;
+  return k.d_table + (size_t)layer * k.beams * k.H * k.max_tiles;
+}
+
+namespace {
+constexpr uint64_t kMagic = 0x31564B4D49505041ull;  // "APPIMKV1"
+}
+
+extern "C" int kv_cache_save(const kv_cache* c, const char* path) {
+  LLM_REQUIRE(c && path, "kv_cache_save: NULL");
+  auto& k = const_cast<kv_cache*>(c)->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  std::ofstream f(path, std::ios::binary);
+  if (!f) return fail(LLM_ERR_IO, std::string("kv_cache_save: cannot open ") + path);
+  const int64_t hdr[8] = {(int64_t)kMagic, k.L, k.beams, k.H, k.D, k.TS, k.max_tiles, k.num_pages};
+  f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
+  f.write(reinterpret_cast<const char*>(k.h_table.data()), k.entries * sizeof(int32_t));
+  std::vector<int32_t> used;
+  for (long long p = 0; p < k.num_pages; ++p)
+    if (k.refcount[p] > 0) used.push_back((int32_t)p);
+  const int64_t nu = (int64_t)used.size();
+  f.write(reinterpret_cast<const char*>(&nu), sizeof(nu));
+  f.write(reinterpret_cast<const char*>(used.data()), used.size() * sizeof(int32_t));
+  const size_t pb = k.page_elems * 2;
+  std::vector<char> buf(pb);
+  LLM_HIP_RET(hipDeviceSynchronize());
+  for (int32_t p : used) {
+    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.k_pool + (size_t)p * pb, pb, hipMemcpyDeviceToHost));
+    f.write(buf.data(), pb);
+    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.v_pool + (size_t)p * pb, pb, hipMemcpyDeviceToHost));
+    f.write(buf.data(), pb);
+  }
+  if (!f) return fail(LLM_ERR_IO, "kv_cache_save: write failed");
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_load(kv_cache* c, const char* path) {
+  LLM_REQUIRE(c && path, "kv_cache_load: NULL");
+  KvCache& k = c->impl;
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return fail(LLM_ERR_IO, std::string("kv_cache_load: cannot open ") + path);
+  int64_t hdr[8];
+  f.read(reinterpret_cast<char*>(hdr), sizeof(hdr));
+  if (!f || hdr[0] != (int64_t)kMagic) return fail(LLM_ERR_IO, "kv_cache_load: bad header");
+  if (hdr[1] != k.L || hdr[2] != k.beams || hdr[3] != k.H || hdr[4] != k.D || hdr[5] != k.TS ||
+      hdr[6] != k.max_tiles || hdr[7] != k.num_pages)
+    return fail(LLM_ERR_INVALID, "kv_cache_load: file geometry differs from this cache");
+  int rc = kv_cache_clear(c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(k.mu);
+  f.read(reinterpret_cast<char*>(k.h_table.data()), k.entries * sizeof(int32_t));
+  int64_t nu = 0;
+  f.read(reinterpret_cast<char*>(&nu), sizeof(nu));
+  if (!f || nu < 0 || nu > k.num_pages) return fail(LLM_ERR_IO, "kv_cache_load: truncated");
+  std::vector<int32_t> used((size_t)nu);
+  f.read(reinterpret_cast<char*>(used.data()), used.size() * sizeof(int32_t));
+  const size_t pb = k.page_elems * 2;
+  std::vector<char> buf(pb);
+  for (int32_t p : used) {
+    f.read(buf.data(), pb);
+    LLM_HIP_RET(hipMemcpy((char*)k.k_pool + (size_t)p * pb, buf.data(), pb, hipMemcpyHostToDevice));
+    f.read(buf.data(), pb);
+    LLM_HIP_RET(hipMemcpy((char*)k.v_pool + (size_t)p * pb, buf.data(), pb, hipMemcpyHostToDevice));
+  }
+  if (!f) return fail(LLM_ERR_IO, "kv_cache_load: truncated page data");
+  // rebuild refcounts / free list from the table
+  std::fill(k.refcount.begin(), k.refcount.end(), 0);
+  for (size_t i = 0; i < k.entries; ++i)
+    if (k.h_table[i] >= 0 && k.h_table[i] < k.num_pages) k.refcount[k.h_table[i]] += 1;
+  k.free_list.clear();
+  for (long long p = k.num_pages - 1; p >= 0; --p)
+    if (k.refcount[p] == 0) k.free_list.push_back((int32_t)p);
+  LLM_HIP_RET(hipMemcpy(k.d_table, k.h_table.data(), k.entries * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+  return LLM_OK;
+}

@@ -1,0 +1,57 @@
+// Internal KV-cache state shared by kv_cache.cpp and the decoder runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "llm_decoder.h"
+
+namespace llm {
+
+struct KvCache {
+  int L = 0, beams = 0, H = 0, D = 0, TS = 0, max_tiles = 0;
+  long long num_pages = 0;
+  size_t page_elems = 0;
+  size_t entries = 0;
+  void* k_pool = nullptr;
+  void* v_pool = nullptr;
+  int32_t* d_table = nullptr;
+  std::vector<int32_t> h_table;     // host mirror = source of truth
+  std::vector<uint8_t> dirty_flag;
+  std::vector<int64_t> dirty;
+  std::vector<int32_t> refcount;
+  std::vector<int32_t> free_list;
+  std::vector<std::pair<int32_t, int32_t>> cow;  // (src page, dst page) copies pending
+  int64_t* d_idx = nullptr;
+  int32_t* d_val = nullptr;
+  int64_t* h_idx = nullptr;
+  int32_t* h_val = nullptr;
+  size_t staging_cap = 0;
+  hipEvent_t staging_done = nullptr;
+  std::mutex mu;
+
+  ~KvCache();
+  int init(int L, int beams, int H, int D, int TS, int max_tiles, long long pages);
+  size_t index(int layer, int beam, int head, int tile) const {
+    return (((size_t)layer * beams + beam) * H + head) * max_tiles + tile;
+  }
+  bool in_range(int layer, int beam, int head, int tile) const;
+  void set_entry(size_t idx, int32_t page);
+  int alloc_page(int32_t* out);
+  void drop_page(int32_t page);
+  // allocate (and, if exclusive, un-share by copy-on-write) the page of a tile
+  int ensure_tile(int layer, int beam, int head, int tile, bool exclusive, int32_t* page);
+  // make the tile of `pos` exist and be exclusive for every layer / head of `beam`
+  int prepare_append(int beam, int pos);
+  // push copy-on-write copies and dirty table entries to the device (stream-ordered)
+  int sync(hipStream_t st);
+};
+
+}  // namespace llm
+
+struct kv_cache;
+llm::KvCache* kv_impl(kv_cache* c);

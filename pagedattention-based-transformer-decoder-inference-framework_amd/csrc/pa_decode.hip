@@ -1,0 +1,390 @@
+// Paged decode attention for gfx950 (CDNA4).
+//
+// Replaces paged_flash_attention_kernel_fused / _overlap
+// (attention/paged_flash_attention_kernel_fused.cu:5-90,
+//  attention/paged_flash_attention_kernel_fused_overlap.cu:6-91) with the
+// intended maths of cpu_paged_attention_forward
+// (attention_cpu/cpu_attention_kernel.cpp:37-129).
+//
+// Decomposition (HBM-bound KV scan, ~1 flop/byte):
+//   * one WAVE per (row b, head h, split s); a split is <= 64 consecutive
+//     pages of that row's page-table row, so its page ids are ONE coalesced
+//     dword load (lane j holds page j) and are broadcast with v_readlane.
+//   * a page (tile) of TS tokens x D fp16 is contiguous; a wave reads it with
+//     TS*D*2/1024 buffer_load_dwordx4 instructions of 1 KiB each (lane l ->
+//     bytes 16l..16l+15): LPT = D/8 lanes hold one token row, TPI = 64/LPT
+//     tokens per instruction.  K and V go straight to VGPRs: each byte is used
+//     by exactly one wave, so an LDS round trip would be pure overhead
+//     (cdna_hip_programming.md, "GEMV / M <= 16" row and Appendix B
+//     "Attention decode").  Two register stages: the next chunk's loads are
+//     in flight while the current chunk is computed.
+//   * invalid pages (table -1, >= num_pages, past the split) use a buffer
+//     descriptor with num_records = 0: the loads return zeros and touch no
+//     memory; their tokens are masked.
+//   * q.k: 8 fp32 FMAs per lane per token row, then a DPP butterfly across the
+//     LPT lanes of the row (quad_perm / row_half_mirror / row_mirror), so every
+//     lane of the row holds the score.
+//   * online softmax per ROW GROUP (lanes sharing lane/LPT): each group keeps
+//     its own running max m, sum l and 8 output dims in registers, so the
+//     inner loop has no cross-row communication; groups are merged once at the
+//     end (flash-decoding within the wave), splits are merged by
+//     pa_merge_kernel (or written directly when there is one split).
+//   * scores are kept in log2 units (q pre-scaled by sm_scale*log2(e)) so
+//     every exponential is one v_exp_f32.
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace llm {
+
+struct PaSplitArgs {
+  const uint8_t* k_pool;
+  const uint8_t* v_pool;
+  const int32_t* page_table;
+  const float* q;
+  float* out;       // DIRECT: final output [B][H][D]
+  float* part_acc;  // [B*H*nsplit][D]
+  float* part_ml;   // [B*H*nsplit][2]
+  const int32_t* beam_ids;
+  const int32_t* context_lens;
+  int B, H, T;
+  int num_pages, num_beams, max_tiles;
+  int pps;     // pages per split (<= 64)
+  int nsplit;  // splits per (b, h)
+  float qscale;
+};
+
+template <int D, int TS, bool DIRECT>
+__global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
+  constexpr int LPT = D / 8;
+  constexpr int TPI = 64 / LPT;
+  constexpr int NI = TS / TPI;
+  constexpr int PAGE_BYTES = TS * D * 2;
+  constexpr int U = (16384 / (2 * PAGE_BYTES)) > 0 ? (16384 / (2 * PAGE_BYTES)) : 1;
+  constexpr int NR = U * NI;
+  static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1, "bad D/TS");
+
+  const int lane = lane_id();
+  const int wid = blockIdx.x * 4 + wave_id_uniform();
+  if (wid >= a.B * a.H * a.nsplit) return;
+  const int s = wid % a.nsplit;
+  const int bh = wid / a.nsplit;
+  const int h = bh % a.H;
+  const int b = bh / a.H;
+  const int r = a.beam_ids ? a.beam_ids[b] : b;
+  int Tb = a.context_lens ? a.context_lens[b] : a.T;
+  Tb = min(max(Tb, 0), a.T);
+  const int ntiles = (Tb + TS - 1) / TS;
+  const int tile0 = s * a.pps;
+  const int count = min(a.pps, ntiles - tile0);
+  const int c = lane % LPT;
+  const int g = lane / LPT;
+
+  if (count <= 0) {
+    if constexpr (DIRECT) {
+      if (lane < LPT) {
+        float* o = a.out + (size_t)bh * D + c * 8;
+        *reinterpret_cast<f32x4*>(o) = f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4*>(o + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    return;
+  }
+
+  // Page ids of this split: lane j holds page j (PageTable::lookup semantics).
+  int pid = -1;
+  if (lane < count && r >= 0 && r < a.num_beams) {
+    const int tile = tile0 + lane;
+    if (tile < a.max_tiles) {
+      pid = a.page_table[((size_t)r * a.H + h) * a.max_tiles + tile];
+      if (pid >= a.num_pages) pid = -1;
+    }
+  }
+
+  // q chunk of this lane (dims c*8 .. c*8+7), pre-scaled into log2 units.
+  float qv[8];
+  {
+    const float* qp = a.q + (size_t)bh * D + c * 8;
+    const f32x4 q0 = *reinterpret_cast<const f32x4*>(qp);
+    const f32x4 q1 = *reinterpret_cast<const f32x4*>(qp + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qv[e] = q0[e] * a.qscale;
+      qv[4 + e] = q1[e] * a.qscale;
+    }
+  }
+
+  float m = kNegSentinel, l = 0.f;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+
+  const uint32_t lane_off = (uint32_t)lane * 16u;
+
+  auto issue = [&](u32x4 (&kk)[NR], u32x4 (&vv)[NR], int p0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = p0 + u;
+      const int pg = __builtin_amdgcn_readlane(pid, min(j, 63));
+      const bool ok = (j < count) && (pg >= 0);
+      const size_t off = (size_t)(ok ? pg : 0) * PAGE_BYTES;
+      const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k_pool + off), (short)0,
+                                                         ok ? PAGE_BYTES : 0, 0x00020000);
+      const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.v_pool + off), (short)0,
+                                                         ok ? PAGE_BYTES : 0, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        kk[u * NI + i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_off + i * 1024, 0, 0);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        vv[u * NI + i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_off + i * 1024, 0, 0);
+    }
+  };
+
+  auto compute = [&](const u32x4 (&kk)[NR], const u32x4 (&vv)[NR], int p0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = p0 + u;
+      const int pg = __builtin_amdgcn_readlane(pid, min(j, 63));
+      const bool ok = (j < count) && (pg >= 0);
+      const int tok_base = (tile0 + j) * TS + g;
+      float sc[NI];
+      bool valid[NI];
+      float mloc = kNegSentinel;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const f16x8 kh = __builtin_bit_cast(f16x8, kk[u * NI + i]);
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d = fmaf(qv[e], (float)kh[e], d);
+        d = group_sum<LPT>(d);
+        valid[i] = ok && (tok_base + i * TPI) < Tb;
+        sc[i] = valid[i] ? d : kNegSentinel;
+        mloc = fmaxf(mloc, sc[i]);
+      }
+      const float mnew = fmaxf(m, mloc);
+      const float corr = __builtin_amdgcn_exp2f(m - mnew);
+      l *= corr;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] *= corr;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const float p = valid[i] ? __builtin_amdgcn_exp2f(sc[i] - mnew) : 0.f;
+        l += p;
+        const f16x8 vh = __builtin_bit_cast(f16x8, vv[u * NI + i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, (float)vh[e], acc[e]);
+      }
+      m = mnew;
+    }
+  };
+
+  const int nchunks = (count + U - 1) / U;
+  u32x4 kA[NR], vA[NR], kB[NR], vB[NR];
+  issue(kA, vA, 0);
+  for (int ch = 0; ch < nchunks; ch += 2) {
+    issue(kB, vB, (ch + 1) * U);  // past-the-end chunks load nothing (num_records 0)
+    compute(kA, vA, ch * U);
+    if (ch + 1 >= nchunks) break;
+    issue(kA, vA, (ch + 2) * U);
+    compute(kB, vB, (ch + 1) * U);
+  }
+
+  // Merge the TPI row groups of the wave (lanes with equal c).
+#pragma unroll
+  for (int off = LPT; off < 64; off <<= 1) {
+    const float mo = __shfl_xor(m, off, 64);
+    const float lo = __shfl_xor(l, off, 64);
+    const float mn = fmaxf(m, mo);
+    const float ca = __builtin_amdgcn_exp2f(m - mn);
+    const float cb = __builtin_amdgcn_exp2f(mo - mn);
+    l = l * ca + lo * cb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float ao = __shfl_xor(acc[e], off, 64);
+      acc[e] = acc[e] * ca + ao * cb;
+    }
+    m = mn;
+  }
+
+  if (lane < LPT) {
+    if constexpr (DIRECT) {
+      const float inv = 1.0f / (l + 1e-6f);
+      float* o = a.out + (size_t)bh * D + c * 8;
+      *reinterpret_cast<f32x4*>(o) = f32x4{acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv};
+      *reinterpret_cast<f32x4*>(o + 4) =
+          f32x4{acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv};
+    } else {
+      float* o = a.part_acc + (size_t)wid * D + c * 8;
+      *reinterpret_cast<f32x4*>(o) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+      if (lane == 0) {
+        a.part_ml[(size_t)wid * 2] = m;
+        a.part_ml[(size_t)wid * 2 + 1] = l;
+      }
+    }
+  }
+}
+
+// Split merge (flash-decoding LSE combine): one wave per (b, h).
+struct PaMergeArgs {
+  const float* part_acc;
+  const float* part_ml;
+  float* out;
+  const int32_t* context_lens;
+  int B, H, D, T, TS, pps, nsplit;
+};
+
+__global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
+  const int lane = lane_id();
+  const int bh = blockIdx.x * 4 + wave_id_uniform();
+  if (bh >= a.B * a.H) return;
+  const int b = bh / a.H;
+  int Tb = a.context_lens ? a.context_lens[b] : a.T;
+  Tb = min(max(Tb, 0), a.T);
+  const int ntiles = (Tb + a.TS - 1) / a.TS;
+  const int ns = min(a.nsplit, (ntiles + a.pps - 1) / a.pps);
+  const float* ml = a.part_ml + (size_t)bh * a.nsplit * 2;
+  float M = kNegSentinel;
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
+  float* o = a.out + (size_t)bh * a.D;
+  if (ns <= 0 || M <= 0.5f * kNegSentinel) {
+    for (int d = lane; d < a.D; d += 64) o[d] = 0.f;
+    return;
+  }
+  float L = 0.f;
+  for (int s = 0; s < ns; ++s) L += ml[2 * s + 1] * __builtin_amdgcn_exp2f(ml[2 * s] - M);
+  const float inv = 1.0f / (L + 1e-6f);
+  const float* pa = a.part_acc + (size_t)bh * a.nsplit * a.D;
+  for (int d = lane; d < a.D; d += 64) {
+    float acc = 0.f;
+    for (int s = 0; s < ns; ++s) acc += pa[(size_t)s * a.D + d] * __builtin_amdgcn_exp2f(ml[2 * s] - M);
+    o[d] = acc * inv;
+  }
+}
+
+namespace {
+
+constexpr int kMinPps = 8;
+constexpr int kMaxPps = 64;
+
+template <int D, int TS>
+hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st) {
+  const int waves = a.B * a.H * a.nsplit;
+  const dim3 grid((waves + 3) / 4), block(256);
+  if (direct)
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, true>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, false>), grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, hipStream_t st) {
+  switch (TS) {
+    case 16: return launch_split<D, 16>(a, direct, st);
+    case 32: return launch_split<D, 32>(a, direct, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+bool supported(int D, int TS) {
+  return (D == 32 || D == 64 || D == 128 || D == 256) && (TS == 16 || TS == 32);
+}
+
+}  // namespace
+
+int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles) {
+  const int ntiles = std::max(1, std::min((T + TS - 1) / TS, max_tiles));
+  const long long bh = std::max(1LL, (long long)B * H);
+  // Enough waves for 256 CUs x ~16 resident waves, in splits of >= kMinPps pages.
+  const long long want_splits = std::max(1LL, (4096 + bh - 1) / bh);
+  long long pps = (ntiles + want_splits - 1) / want_splits;
+  pps = std::max<long long>(pps, kMinPps);
+  pps = std::min<long long>(pps, kMaxPps);
+  return (int)pps;
+}
+
+}  // namespace llm
+
+using namespace llm;
+
+extern "C" int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles) {
+  if (B < 0 || H <= 0 || T < 0 || page_size <= 0 || max_tiles <= 0) return -1;
+  return pa_pages_per_split(B, H, T, page_size, max_tiles);
+}
+
+extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
+                                            int pages_per_split) {
+  if (B <= 0 || H <= 0 || D <= 0 || max_tiles <= 0) return 0;
+  const int pps = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps) : kMinPps;
+  const size_t nsplit = (size_t)(max_tiles + pps - 1) / pps;
+  return (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
+}
+
+extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
+                         const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
+                         int D, int T, float sm_scale, int pages_per_split, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  LLM_REQUIRE(kv != nullptr, "pa_decode: kv view is NULL");
+  LLM_REQUIRE(B >= 0 && H > 0 && D > 0 && T >= 0, "pa_decode: bad B/H/D/T");
+  if (B == 0) return LLM_OK;
+  LLM_REQUIRE(q != nullptr && out != nullptr, "pa_decode: q/out NULL");
+  LLM_REQUIRE(kv->k_pool && kv->v_pool && kv->page_table, "pa_decode: kv pointers NULL");
+  LLM_REQUIRE(kv->kv_dtype == LLM_F16, "pa_decode: only fp16 KV pools are supported");
+  LLM_REQUIRE(kv->num_heads == H, "pa_decode: H != kv->num_heads");
+  LLM_REQUIRE(kv->head_dim == D, "pa_decode: D != kv->head_dim");
+  LLM_REQUIRE(kv->num_pages > 0 && kv->num_beams > 0 && kv->max_tiles > 0,
+              "pa_decode: empty kv view");
+  if (!supported(D, kv->page_size))
+    return fail(LLM_ERR_UNSUPPORTED, "pa_decode: unsupported head_dim/page_size (D in "
+                                     "{32,64,128,256}, page_size in {16,32})");
+  LLM_REQUIRE((long long)kv->num_pages * kv->page_size * D * 2 < (1LL << 47),
+              "pa_decode: pool too large");
+  const int TS = kv->page_size;
+  const int ntiles_max = std::max(1, (T + TS - 1) / TS);
+  int pps = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps)
+                                : pa_pages_per_split(B, H, T, TS, kv->max_tiles);
+  const int nsplit = (ntiles_max + pps - 1) / pps;
+  const bool direct = nsplit <= 1;
+
+  PaSplitArgs a{};
+  a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
+  a.v_pool = static_cast<const uint8_t*>(kv->v_pool);
+  a.page_table = kv->page_table;
+  a.q = q;
+  a.out = out;
+  a.beam_ids = beam_ids;
+  a.context_lens = context_lens;
+  a.B = B;
+  a.H = H;
+  a.T = T;
+  a.num_pages = kv->num_pages;
+  a.num_beams = kv->num_beams;
+  a.max_tiles = kv->max_tiles;
+  a.pps = pps;
+  a.nsplit = direct ? 1 : nsplit;
+  a.qscale = sm_scale * kLog2e;
+  if (!direct) {
+    const size_t need = (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
+    LLM_REQUIRE(workspace != nullptr && workspace_bytes >= need,
+                "pa_decode: workspace too small (see pa_decode_workspace_bytes)");
+    a.part_acc = static_cast<float*>(workspace);
+    a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
+  }
+  hipStream_t st = as_stream(stream);
+  hipError_t e;
+  switch (D) {
+    case 32: e = dispatch_ts<32>(a, TS, direct, st); break;
+    case 64: e = dispatch_ts<64>(a, TS, direct, st); break;
+    case 128: e = dispatch_ts<128>(a, TS, direct, st); break;
+    default: e = dispatch_ts<256>(a, TS, direct, st); break;
+  }
+  if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
+  if (!direct) {
+    PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, TS, pps, nsplit};
+    hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
+    LLM_HIP_RET(hipGetLastError());
+  }
+  return LLM_OK;
+}

@@ -1,0 +1,285 @@
+// Row-wise decoder glue kernels: LayerNorm (+ fused int8 quantisation),
+// per-row int8 quantisation, embedding gather, KV append into pages, argmax.
+// All are one workgroup per row, vectorised 16 B per lane where the row allows.
+#include "common.hpp"
+#include "row_ops.hpp"
+
+namespace llm {
+
+constexpr int kRowThreads = 256;
+
+__device__ __forceinline__ float block_reduce_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) t += sh[i];  // fixed order: deterministic
+  return t;
+}
+
+__device__ __forceinline__ float block_reduce_max(float v, float* sh) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  float t = sh[0];
+  const int nw = blockDim.x >> 6;
+  for (int i = 1; i < nw; ++i) t = fmaxf(t, sh[i]);
+  return t;
+}
+
+// int8_quant.cpp:5-13,59-64: scale = 127/(absmax + 1e-6), q = clamp(round(x*scale)).
+__device__ __forceinline__ int8_t quant1(float x, float scale) {
+  float y = roundf(__fmul_rn(x, scale));
+  y = fminf(fmaxf(y, -128.f), 127.f);
+  return (int8_t)(int)y;
+}
+
+// Quantise one row held by the block (values in `vals`, VPT per thread,
+// element index i = threadIdx.x + k*blockDim.x).
+__global__ __launch_bounds__(kRowThreads) void quantize_rows_kernel(const float* __restrict__ x,
+                                                                    int cols, int8_t* __restrict__ q,
+                                                                    float* __restrict__ inv_scale) {
+  __shared__ float sh[kRowThreads / 64];
+  const int r = blockIdx.x;
+  const float* xr = x + (size_t)r * cols;
+  float am = 0.f;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) am = fmaxf(am, fabsf(xr[i]));
+  am = block_reduce_max(am, sh);
+  const float scale = 127.f / (am + 1e-6f);
+  int8_t* qr = q + (size_t)r * cols;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) qr[i] = quant1(xr[i], scale);
+  if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
+}
+
+// LayerNorm<T>::forward (decoder/layer_norm.hpp:20-37): biased variance,
+// inv_std = 1.0/sqrt(var + eps), out = (x - mean) * inv_std * gamma + beta
+// (left-to-right, not contracted), then optional per-row int8 quantisation.
+__global__ __launch_bounds__(kRowThreads) void layernorm_quant_kernel(
+    const float* __restrict__ x, int cols, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
+    float* __restrict__ inv_scale) {
+  extern __shared__ __attribute__((aligned(16))) float row[];  // cols floats
+  __shared__ float sh[kRowThreads / 64];
+  const int r = blockIdx.x;
+  const float* xr = x + (size_t)r * cols;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) {
+    const float v = xr[i];
+    row[i] = v;
+    s += v;
+  }
+  const float mean = block_reduce_sum(s, sh) / (float)cols;
+  float vs = 0.f;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) {
+    const float d = row[i] - mean;
+    vs = fmaf(d, d, vs);
+  }
+  const float var = block_reduce_sum(vs, sh) / (float)cols;
+  const float inv_std = (float)(1.0 / (double)sqrtf(var + eps));
+  float am = 0.f;
+  for (int i = threadIdx.x; i < cols; i += blockDim.x) {
+    float y = __fmul_rn(__fmul_rn(row[i] - mean, inv_std), gamma[i]);
+    y = __fadd_rn(y, beta[i]);
+    row[i] = y;
+    am = fmaxf(am, fabsf(y));
+    if (out) out[(size_t)r * cols + i] = y;
+  }
+  if (q) {
+    am = block_reduce_max(am, sh);
+    const float scale = 127.f / (am + 1e-6f);
+    for (int i = threadIdx.x; i < cols; i += blockDim.x) q[(size_t)r * cols + i] = quant1(row[i], scale);
+    if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
+  }
+}
+
+// Argmax per row, first maximum wins (std::max_element).
+__global__ __launch_bounds__(kRowThreads) void argmax_kernel(const float* __restrict__ logits,
+                                                             int V, int32_t* __restrict__ out,
+                                                             int32_t* __restrict__ out2,
+                                                             int out2_stride) {
+  __shared__ float shv[kRowThreads];
+  __shared__ int shi[kRowThreads];
+  const int r = blockIdx.x;
+  const float* l = logits + (size_t)r * V;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    const float v = l[i];
+    if (v > best) { best = v; bi = i; }  // strided scan: first index per thread
+  }
+  shv[threadIdx.x] = best;
+  shi[threadIdx.x] = bi;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const float v2 = shv[threadIdx.x + s];
+      const int i2 = shi[threadIdx.x + s];
+      if (v2 > shv[threadIdx.x] || (v2 == shv[threadIdx.x] && i2 < shi[threadIdx.x])) {
+        shv[threadIdx.x] = v2;
+        shi[threadIdx.x] = i2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int idx = shi[0] == 0x7fffffff ? 0 : shi[0];
+    out[r] = idx;
+    if (out2) out2[(size_t)r * out2_stride] = idx;
+  }
+}
+
+// x[b] = float(E[tok[b]]) (TokenEmbedding::forward, decoder/token_embedding.hpp:19-26).
+__global__ __launch_bounds__(kRowThreads) void embed_kernel(const _Float16* __restrict__ E,
+                                                            const int32_t* __restrict__ tok,
+                                                            int hid, int V,
+                                                            float* __restrict__ x) {
+  const int b = blockIdx.x;
+  int t = tok[b];
+  t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+  const _Float16* e = E + (size_t)t * hid;
+  float* xr = x + (size_t)b * hid;
+  for (int i = threadIdx.x; i < hid; i += blockDim.x) xr[i] = (float)e[i];
+}
+
+// Append this step's K and V (fp32 rows of the qkv projection, layout
+// [b][q|k|v][H][D]) into the pages of position pos[b]
+// (KVTileCache::get_write_ptr, kv_cache/kv_tile_cache.hpp:28-34).
+__global__ __launch_bounds__(kRowThreads) void kv_append_kernel(
+    const float* __restrict__ qkv, int H, int D, const int32_t* __restrict__ pos,
+    const int32_t* __restrict__ page_table, int num_beams, int max_tiles, int TS, int num_pages,
+    _Float16* __restrict__ k_pool, _Float16* __restrict__ v_pool) {
+  const int b = blockIdx.x;
+  const int hid = H * D;
+  const int p = pos[b];
+  const int tile = p / TS, row = p % TS;
+  const float* src = qkv + (size_t)b * 3 * hid;
+  for (int i = threadIdx.x; i < hid; i += blockDim.x) {
+    const int h = i / D, d = i % D;
+    if (b >= num_beams || tile >= max_tiles) continue;
+    const int page = page_table[((size_t)b * H + h) * max_tiles + tile];
+    if (page < 0 || page >= num_pages) continue;
+    const size_t off = ((size_t)page * TS + row) * D + d;
+    k_pool[off] = (_Float16)src[hid + i];
+    v_pool[off] = (_Float16)src[2 * hid + i];
+  }
+}
+
+// page_table[idx[i]] = val[i] (device half of PageTable sync).
+__global__ void scatter_i32_kernel(int32_t* __restrict__ dst, const int64_t* __restrict__ idx,
+                                   const int32_t* __restrict__ val, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[idx[i]] = val[i];
+}
+
+// Seeded random fp16 fill (synthetic KV contexts): splitmix64 -> ~N(0,1)*scale
+// via the sum of 4 uniforms (Irwin-Hall), cheap and deterministic.
+__global__ void fill_random_f16_kernel(_Float16* __restrict__ p, size_t n, uint64_t seed,
+                                       float scale) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    float u = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u += (float)((z >> (16 * k)) & 0xFFFF) * (1.0f / 65536.0f);
+    p[i] = (_Float16)((u - 2.0f) * 1.7320508f * scale);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers (internal)
+// ---------------------------------------------------------------------------
+hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(quantize_rows_kernel, dim3(rows), dim3(kRowThreads), 0, st, x, cols, q, inv);
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
+                                  const float* b, float eps, float* out, int8_t* q, float* inv,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
+                     (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv);
+  return hipGetLastError();
+}
+
+hipError_t launch_argmax(const float* logits, int rows, int V, int32_t* out, int32_t* out2,
+                         int out2_stride, hipStream_t st) {
+  hipLaunchKernelGGL(argmax_kernel, dim3(rows), dim3(kRowThreads), 0, st, logits, V, out, out2,
+                     out2_stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_embed(const void* E, const int32_t* tok, int rows, int hid, int V, float* x,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(embed_kernel, dim3(rows), dim3(kRowThreads), 0, st,
+                     static_cast<const _Float16*>(E), tok, hid, V, x);
+  return hipGetLastError();
+}
+
+hipError_t launch_kv_append(const float* qkv, int rows, int H, int D, const int32_t* pos,
+                            const int32_t* page_table, int num_beams, int max_tiles, int TS,
+                            int num_pages, void* k_pool, void* v_pool, hipStream_t st) {
+  hipLaunchKernelGGL(kv_append_kernel, dim3(rows), dim3(kRowThreads), 0, st, qkv, H, D, pos,
+                     page_table, num_beams, max_tiles, TS, num_pages,
+                     static_cast<_Float16*>(k_pool), static_cast<_Float16*>(v_pool));
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* val, int n,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_i32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dst, idx, val, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_random_f16(void* p, size_t n, uint64_t seed, float scale, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(fill_random_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     static_cast<_Float16*>(p), n, seed, scale);
+  return hipGetLastError();
+}
+
+}  // namespace llm
+
+using namespace llm;
+
+extern "C" int quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv_scale,
+                             void* stream) {
+  LLM_REQUIRE(rows >= 0 && cols > 0, "quantize_rows: bad shape");
+  if (rows == 0) return LLM_OK;
+  LLM_REQUIRE(x && q && inv_scale, "quantize_rows: NULL pointer");
+  LLM_HIP_RET(launch_quantize_rows(x, rows, cols, q, inv_scale, as_stream(stream)));
+  return LLM_OK;
+}
+
+extern "C" int layernorm_quant(const float* x, int rows, int cols, const float* gamma,
+                               const float* beta, float eps, float* out, int8_t* q,
+                               float* inv_scale, void* stream) {
+  LLM_REQUIRE(rows >= 0 && cols > 0, "layernorm_quant: bad shape");
+  if (rows == 0) return LLM_OK;
+  LLM_REQUIRE(x && gamma && beta, "layernorm_quant: NULL pointer");
+  LLM_REQUIRE((q == nullptr) == (inv_scale == nullptr), "layernorm_quant: q and inv_scale go together");
+  LLM_REQUIRE(out || q, "layernorm_quant: no output requested");
+  LLM_REQUIRE(cols <= 16384, "layernorm_quant: cols > 16384 (LDS row buffer)");
+  LLM_HIP_RET(launch_layernorm_quant(x, rows, cols, gamma, beta, eps, out, q, inv_scale,
+                                     as_stream(stream)));
+  return LLM_OK;
+}
+
+extern "C" int argmax_rows(const float* logits, int rows, int V, int32_t* out, void* stream) {
+  LLM_REQUIRE(rows >= 0 && V > 0, "argmax_rows: bad shape");
+  if (rows == 0) return LLM_OK;
+  LLM_REQUIRE(logits && out, "argmax_rows: NULL pointer");
+  LLM_HIP_RET(launch_argmax(logits, rows, V, out, nullptr, 0, as_stream(stream)));
+  return LLM_OK;
+}

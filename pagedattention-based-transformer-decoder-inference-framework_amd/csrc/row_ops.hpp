@@ -1,0 +1,27 @@
+// Internal launchers of csrc/row_ops.hip (used by the decoder runtime).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace llm {
+
+hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv,
+                                hipStream_t st);
+hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
+                                  const float* b, float eps, float* out, int8_t* q, float* inv,
+                                  hipStream_t st);
+hipError_t launch_argmax(const float* logits, int rows, int V, int32_t* out, int32_t* out2,
+                         int out2_stride, hipStream_t st);
+hipError_t launch_embed(const void* E, const int32_t* tok, int rows, int hid, int V, float* x,
+                        hipStream_t st);
+hipError_t launch_kv_append(const float* qkv, int rows, int H, int D, const int32_t* pos,
+                            const int32_t* page_table, int num_beams, int max_tiles, int TS,
+                            int num_pages, void* k_pool, void* v_pool, hipStream_t st);
+hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* val, int n,
+                              hipStream_t st);
+hipError_t launch_fill_random_f16(void* p, size_t n, uint64_t seed, float scale, hipStream_t st);
+
+}  // namespace llm

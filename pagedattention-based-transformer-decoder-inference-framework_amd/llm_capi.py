@@ -1,0 +1,236 @@
+"""ctypes binding of the C ABI (include/llm_decoder.h) exported by
+libllm_decoder_hip.so.
+
+This is the thin Python face of the drop-in boundary used by the tests and
+bench.py to call individual entry points (pa_decode, i8_gemm, ...) on device
+buffers they own (torch tensors, via data_ptr()).  The decoder-level surface
+of the reference (CUDADecoder / INT8Decoder / PageTable / KVTileCache) is the
+pybind11 module ``llm_decoder`` built next to this file.
+
+There is no fallback: if the HIP library is missing, load() raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "libllm_decoder_hip.so"
+
+LLM_OK, LLM_ERR_INVALID, LLM_ERR_UNSUPPORTED, LLM_ERR_HIP, LLM_ERR_OOM, LLM_ERR_IO = range(6)
+LLM_F16, LLM_I8, LLM_F32 = 0, 1, 2
+LLM_ACT_NONE, LLM_ACT_RELU, LLM_ACT_GELU = 0, 1, 2
+
+c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+c_ll = ctypes.c_longlong
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+class PaKvView(ctypes.Structure):
+    _fields_ = [("k_pool", c_void_p), ("v_pool", c_void_p), ("page_table", c_void_p),
+                ("num_pages", ctypes.c_int32), ("page_size", ctypes.c_int32),
+                ("head_dim", ctypes.c_int32), ("num_beams", ctypes.c_int32),
+                ("num_heads", ctypes.c_int32), ("max_tiles", ctypes.c_int32),
+                ("kv_dtype", ctypes.c_int32)]
+
+
+class LlmError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"[llm status {status}] {msg}")
+        self.status = status
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "llm_last_error": (ctypes.c_char_p, []),
+    "llm_abi_version": (c_int, []),
+    "pa_decode_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "pa_decode_pages_per_split": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "pa_decode": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_size_t,
+                          c_void_p]),
+    "gemm_packed_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "gemm_pack_weights": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "i8_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                        c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "f16_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                         c_int, c_void_p]),
+    "lm_head": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "argmax_rows": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "quantize_rows": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "layernorm_quant": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p,
+                                c_void_p, c_void_p, c_void_p]),
+    "kv_cache_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_ll,
+                                ctypes.POINTER(c_void_p)]),
+    "kv_cache_destroy": (None, [c_void_p]),
+    "kv_cache_view": (c_int, [c_void_p, c_int, ctypes.POINTER(PaKvView)]),
+    "kv_cache_num_pages": (c_ll, [c_void_p]),
+    "kv_cache_free_pages": (c_ll, [c_void_p]),
+    "kv_cache_assign": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int]),
+    "kv_cache_lookup": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
+    "kv_cache_remove": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
+    "kv_cache_register_tile": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_i32p]),
+    "kv_cache_reserve": (c_int, [c_void_p, c_int, c_int]),
+    "kv_cache_fork": (c_int, [c_void_p, c_int, c_int]),
+    "kv_cache_release": (c_int, [c_void_p, c_int]),
+    "kv_cache_clear": (c_int, [c_void_p]),
+    "kv_cache_sync": (c_int, [c_void_p, c_void_p]),
+    "kv_cache_write_tokens": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "kv_cache_k_pool": (c_void_p, [c_void_p]),
+    "kv_cache_v_pool": (c_void_p, [c_void_p]),
+    "kv_cache_page_table": (c_void_p, [c_void_p, c_int]),
+    "kv_cache_save": (c_int, [c_void_p, ctypes.c_char_p]),
+    "kv_cache_load": (c_int, [c_void_p, ctypes.c_char_p]),
+}
+
+_lib = None
+
+
+def declared_symbols() -> list[str]:
+    """Every function name declared in include/llm_decoder.h."""
+    import re
+    hdr = (HERE.parent / "include" / "llm_decoder.h").read_text()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    names = re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", hdr)
+    skip = {"if", "for", "while", "sizeof", "return", "defined"}
+    return sorted({n for n in names if n not in skip})
+
+
+def load(path: str | Path | None = None) -> ctypes.CDLL:
+    """Load the HIP C-ABI library (raises if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise FileNotFoundError(
+            f"{p} not found: build it with `make -C {HERE}` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        if not hasattr(lib, name):  # export completeness is asserted by tests/test_capi_symbols.py
+            continue
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int) -> None:
+    if status != LLM_OK:
+        msg = load().llm_last_error()
+        raise LlmError(status, msg.decode() if msg else "")
+
+
+def stream_ptr(stream=None):
+    """hipStream_t of a torch stream (current stream by default) as void*."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def kv_view(k_pool, v_pool, page_table, *, num_beams=None) -> PaKvView:
+    """View over torch device tensors k/v [num_pages][ts][D] fp16 and page
+    table int32 [num_beams][H][max_tiles]."""
+    nb, H, mt = page_table.shape
+    v = PaKvView()
+    v.k_pool, v.v_pool, v.page_table = k_pool.data_ptr(), v_pool.data_ptr(), page_table.data_ptr()
+    v.num_pages, v.page_size, v.head_dim = k_pool.shape[0], k_pool.shape[1], k_pool.shape[2]
+    v.num_beams, v.num_heads, v.max_tiles = num_beams or nb, H, mt
+    v.kv_dtype = LLM_F16
+    return v
+
+
+def pa_decode(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_lens=None,
+              sm_scale=1.0, pages_per_split=0, out=None, stream=None):
+    """Paged decode attention on torch device tensors; returns out [B][H][D] fp32."""
+    import torch
+    lib = load()
+    B, H, D = q.shape
+    if out is None:
+        out = torch.empty((B, H, D), dtype=torch.float32, device=q.device)
+    view = kv_view(k_pool, v_pool, page_table)
+    ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, page_table.shape[2], pages_per_split)
+    ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=q.device)
+    check(lib.pa_decode(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids), ptr(context_lens),
+                        B, H, D, T, sm_scale, pages_per_split, ptr(ws), ws_bytes,
+                        stream_ptr(stream)))
+    return out
+
+
+def pack_weights(W, dtype: int, stream=None):
+    """Repack a device [K][N] int8 / fp16 weight into MFMA fragment order."""
+    import torch
+    lib = load()
+    K, N = W.shape
+    nbytes = lib.gemm_packed_bytes(dtype, K, N)
+    P = torch.empty(nbytes, dtype=torch.uint8, device=W.device)
+    check(lib.gemm_pack_weights(dtype, ptr(W), ptr(P), K, N, stream_ptr(stream)))
+    return P
+
+
+def i8_gemm(A, W_packed, N, *, sa=None, sw=None, bias=None, act=0, want_acc=True, stream=None):
+    import torch
+    lib = load()
+    M, K = A.shape
+    acc = torch.empty((M, N), dtype=torch.int32, device=A.device) if want_acc else None
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    check(lib.i8_gemm(ptr(A), A.stride(0), ptr(W_packed), ptr(acc), ptr(C), M, N, K, ptr(sa),
+                      ptr(sw), ptr(bias), act, stream_ptr(stream)))
+    return acc, C
+
+
+def f16_gemm(A, W_packed, N, *, bias=None, act=0, stream=None):
+    import torch
+    lib = load()
+    M, K = A.shape
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    check(lib.f16_gemm(ptr(A), A.stride(0), ptr(W_packed), ptr(C), M, N, K, ptr(bias), act,
+                       stream_ptr(stream)))
+    return C
+
+
+def lm_head(x, E, stream=None):
+    import torch
+    lib = load()
+    M, K = x.shape
+    V = E.shape[0]
+    out = torch.empty((M, V), dtype=torch.float32, device=x.device)
+    check(lib.lm_head(ptr(x), ptr(E), ptr(out), M, V, K, stream_ptr(stream)))
+    return out
+
+
+def argmax_rows(logits, stream=None):
+    import torch
+    lib = load()
+    R, V = logits.shape
+    out = torch.empty(R, dtype=torch.int32, device=logits.device)
+    check(lib.argmax_rows(ptr(logits), R, V, ptr(out), stream_ptr(stream)))
+    return out
+
+
+def quantize_rows(x, stream=None):
+    import torch
+    lib = load()
+    R, C = x.shape
+    q = torch.empty((R, C), dtype=torch.int8, device=x.device)
+    s = torch.empty(R, dtype=torch.float32, device=x.device)
+    check(lib.quantize_rows(ptr(x), R, C, ptr(q), ptr(s), stream_ptr(stream)))
+    return q, s
+
+
+def layernorm_quant(x, gamma, beta, eps=1e-5, quant=True, stream=None):
+    import torch
+    lib = load()
+    R, C = x.shape
+    out = torch.empty((R, C), dtype=torch.float32, device=x.device)
+    q = torch.empty((R, C), dtype=torch.int8, device=x.device) if quant else None
+    s = torch.empty(R, dtype=torch.float32, device=x.device) if quant else None
+    check(lib.layernorm_quant(ptr(x), R, C, ptr(gamma), ptr(beta), eps, ptr(out), ptr(q), ptr(s),
+                              stream_ptr(stream)))
+    return out, q, s

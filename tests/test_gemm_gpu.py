@@ -1,0 +1,121 @@
+"""Parity of the MFMA GEMMs and row kernels (via the C ABI) against the oracle.
+
+INT8: int32 accumulators bit-exact (north_star); the fp32 epilogue uses the
+same float operations as the oracle (mul, then add, round-to-nearest, not
+contracted) and is compared bit-exactly for act none/relu, 1e-6 rel for GELU.
+FP16 GEMM / LM head: fp32 reference, 1e-3 / 1e-5 rel."""
+import numpy as np
+import pytest
+
+from _util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("M,K,N", [
+    (1, 256, 1024), (16, 768, 2304), (64, 2048, 6144), (64, 8192, 2048), (37, 256, 48),
+    (130, 512, 256), (64, 256, 16), (5, 64, 32),
+])
+def test_i8_gemm_exact(gpu, oracle, M, K, N):
+    import llm_capi
+    rng = np.random.default_rng(M * 7 + K + N)
+    A = rng.integers(-128, 128, (M, K), dtype=np.int8)
+    W = rng.integers(-128, 128, (K, N), dtype=np.int8)
+    sa = rng.uniform(1e-3, 1e-2, M).astype(np.float32)
+    sw = rng.uniform(1e-3, 1e-2, N).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    Wp = llm_capi.pack_weights(_dev(W), llm_capi.LLM_I8)
+    for act in (0, 1, 2):
+        acc, C = llm_capi.i8_gemm(_dev(A), Wp, N, sa=_dev(sa), sw=_dev(sw), bias=_dev(bias), act=act)
+        ref_acc, ref_C = oracle.i8_gemm(A, W, sa, sw, bias, act)
+        np.testing.assert_array_equal(acc.cpu().numpy(), ref_acc)
+        if act < 2:
+            np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
+        else:
+            np.testing.assert_allclose(C.cpu().numpy(), ref_C, rtol=1e-6, atol=1e-6)
+
+
+def test_i8_gemm_no_scales(gpu, oracle):
+    import llm_capi
+    rng = np.random.default_rng(3)
+    A = rng.integers(-128, 128, (8, 128), dtype=np.int8)
+    W = rng.integers(-128, 128, (128, 64), dtype=np.int8)
+    Wp = llm_capi.pack_weights(_dev(W), llm_capi.LLM_I8)
+    acc, C = llm_capi.i8_gemm(_dev(A), Wp, 64)
+    ref = A.astype(np.int64) @ W.astype(np.int64)
+    np.testing.assert_array_equal(acc.cpu().numpy(), ref)
+    np.testing.assert_array_equal(C.cpu().numpy(), ref.astype(np.float32))
+
+
+@pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (64, 2048, 512), (3, 96, 48), (80, 256, 64)])
+def test_f16_gemm(gpu, M, K, N):
+    import llm_capi
+    rng = np.random.default_rng(K + N)
+    A = rng.standard_normal((M, K)).astype(np.float16)
+    W = (0.05 * rng.standard_normal((K, N))).astype(np.float16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    Wp = llm_capi.pack_weights(_dev(W), llm_capi.LLM_F16)
+    for act in (0, 1, 2):
+        C = llm_capi.f16_gemm(_dev(A), Wp, N, bias=_dev(bias), act=act).cpu().numpy()
+        ref = A.astype(np.float64) @ W.astype(np.float64) + bias
+        if act == 1:
+            ref = np.maximum(ref, 0)
+        elif act == 2:
+            from scipy.special import erf
+            ref = 0.5 * ref * (1 + erf(ref / np.sqrt(2)))
+        assert rel_err(C, ref) < 1e-3
+
+
+@pytest.mark.parametrize("M,V,K", [(64, 50257, 2048), (1, 1000, 256), (16, 50257, 768), (70, 333, 64)])
+def test_lm_head(gpu, M, V, K):
+    import llm_capi
+    rng = np.random.default_rng(V + K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    E = rng.standard_normal((V, K)).astype(np.float16)
+    out = llm_capi.lm_head(_dev(x), _dev(E)).cpu().numpy()
+    ref = x.astype(np.float64) @ E.astype(np.float64).T
+    assert rel_err(out, ref) < 2e-6
+
+
+def test_argmax_first_wins(gpu):
+    import llm_capi
+    rng = np.random.default_rng(0)
+    L = rng.standard_normal((9, 50257)).astype(np.float32)
+    L[1, 10] = L[1, 20] = 100.0  # tie: first index wins
+    L[2, :] = 0.0
+    L[3, 50256] = 1e9
+    out = llm_capi.argmax_rows(_dev(L)).cpu().numpy()
+    np.testing.assert_array_equal(out, np.argmax(L, axis=1))
+    assert out[1] == 10 and out[2] == 0
+
+
+def test_quantize_rows_exact(gpu, oracle):
+    import llm_capi
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal((33, 2048)) * 3).astype(np.float32)
+    x[0] = 0.0
+    x[1, :4] = [0.5, -0.5, 1.5, 127.0]
+    q, s = llm_capi.quantize_rows(_dev(x))
+    qr, sr = oracle.quantize_rows(x)
+    np.testing.assert_array_equal(q.cpu().numpy(), qr)
+    np.testing.assert_array_equal(s.cpu().numpy(), sr)
+
+
+def test_layernorm_quant(gpu, oracle):
+    import llm_capi
+    rng = np.random.default_rng(4)
+    x = (rng.standard_normal((20, 2048)) * 2 + 0.5).astype(np.float32)
+    g = (1 + 0.1 * rng.standard_normal(2048)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(2048)).astype(np.float32)
+    out, q, s = llm_capi.layernorm_quant(_dev(x), _dev(g), _dev(b))
+    ref = oracle.layer_norm(x, g, b)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    qr, sr = oracle.quantize_rows(ref)
+    dq = np.abs(q.cpu().numpy().astype(np.int32) - qr.astype(np.int32))
+    assert dq.max() <= 1 and (dq > 0).mean() < 1e-3
+    np.testing.assert_allclose(s.cpu().numpy(), sr, rtol=1e-5)

@@ -1,0 +1,172 @@
+"""Parity of the HIP paged decode attention (pa_decode, via the C ABI) against
+the CPU oracle and the reference-built golden fixtures.
+
+Tolerance (north_star): page-table indexing is bit-exact by construction (a
+wrong page changes the output by O(1)); fp16-KV / fp32-accumulate outputs must
+agree within 1e-3 relative (max-abs error / max-abs reference)."""
+import numpy as np
+import pytest
+
+from _util import GOLDEN, load_attn_fixture, rel_err, tiles_to_pool
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-3
+
+GPU_CASES = ["c1_base", "c1_missing", "beam_route", "temp07", "d128", "ragged_tail", "ts32",
+             "all_missing"]
+
+
+def _dev(a, dtype=None):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+@pytest.mark.parametrize("name", GPU_CASES)
+@pytest.mark.parametrize("pps", [0, 1, 3])
+def test_pa_decode_matches_golden(gpu, oracle, name, pps):
+    import llm_capi
+    f = load_attn_fixture(name)
+    assert f["top_k"] == 0 and f["top_p"] >= 1.0 and f["eos"] < 0
+    k_pool, v_pool, pt = tiles_to_pool(f["k"], f["v"], f["present"])
+    bi = None if f["beam_ids"] is None else _dev(f["beam_ids"])
+    out = llm_capi.pa_decode(_dev(f["q"]), _dev(k_pool), _dev(v_pool), _dev(pt), T=f["T"],
+                             beam_ids=bi, sm_scale=1.0 / f["temperature"] ** 2,
+                             pages_per_split=pps).cpu().numpy()
+    if name == "all_missing":
+        np.testing.assert_array_equal(out, np.zeros_like(out))
+    else:
+        assert rel_err(out, f["out"]) < RTOL, rel_err(out, f["out"])
+    ref = oracle.paged_attention(f["q"], k_pool.astype(np.float32), v_pool.astype(np.float32), pt,
+                                 T=f["T"], beam_ids=f["beam_ids"], temperature=f["temperature"])
+    if name != "all_missing":
+        assert rel_err(out, ref) < RTOL
+
+
+def _random_case(rng, B, H, D, T, ts, *, num_beams=None, max_tiles=None, missing_frac=0.0):
+    num_beams = num_beams or B
+    nt = (T + ts - 1) // ts
+    max_tiles = max_tiles or nt
+    num_pages = num_beams * H * nt + 5
+    scale = D ** -0.25
+    q = (rng.standard_normal((B, H, D)) * scale).astype(np.float32)
+    k_pool = (rng.standard_normal((num_pages, ts, D)) * scale).astype(np.float16)
+    v_pool = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
+    perm = rng.permutation(num_pages)[: num_beams * H * nt].astype(np.int32)
+    pt = np.full((num_beams, H, max_tiles), -1, np.int32)
+    pt[:, :, :nt] = perm.reshape(num_beams, H, nt)
+    if missing_frac:
+        mask = rng.random(pt[:, :, :nt].shape) < missing_frac
+        pt[:, :, :nt][mask] = -1
+    return q, k_pool, v_pool, pt
+
+
+@pytest.mark.parametrize("B,H,D,T,ts", [
+    (16, 12, 64, 2048, 16),   # C2 attention shape
+    (3, 4, 128, 1000, 16),    # ragged tail, D=128
+    (2, 2, 256, 300, 16),
+    (5, 3, 32, 257, 32),
+    (4, 2, 128, 4096, 32),
+])
+def test_pa_decode_random_vs_oracle(gpu, oracle, B, H, D, T, ts):
+    import llm_capi
+    rng = np.random.default_rng(B * 1000 + T)
+    q, kp, vp, pt = _random_case(rng, B, H, D, T, ts, missing_frac=0.02)
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T)
+    for pps in (0, 8, 64):
+        out = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T,
+                                 pages_per_split=pps).cpu().numpy()
+        assert rel_err(out, ref) < RTOL, (pps, rel_err(out, ref))
+
+
+def test_pa_decode_ragged_context_and_beams(gpu, oracle):
+    import llm_capi
+    rng = np.random.default_rng(11)
+    B, H, D, T, ts = 6, 4, 128, 700, 16
+    q, kp, vp, pt = _random_case(rng, B, H, D, T, ts, num_beams=3, max_tiles=50)
+    beam_ids = np.array([2, 0, 1, 1, 0, 2], np.int32)
+    lens = np.array([700, 1, 0, 17, 512, 333], np.int32)
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T,
+                                 beam_ids=beam_ids, context_lens=lens)
+    for pps in (0, 4, 64):
+        out = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T,
+                                 beam_ids=_dev(beam_ids), context_lens=_dev(lens),
+                                 pages_per_split=pps).cpu().numpy()
+        assert rel_err(out, ref) < RTOL
+        np.testing.assert_array_equal(out[2], 0.0)  # empty context -> zeros
+
+
+def test_pa_decode_softmax_spike(gpu, oracle):
+    """Force the online-softmax rescale: a key in a late page dominates."""
+    import llm_capi
+    rng = np.random.default_rng(5)
+    B, H, D, T, ts = 2, 2, 128, 1024, 16
+    q, kp, vp, pt = _random_case(rng, B, H, D, T, ts)
+    # put a strongly aligned key at token 900 of (0,0) and token 17 of (1,1)
+    for (b, h, t) in [(0, 0, 900), (1, 1, 17)]:
+        page = pt[b, h, t // ts]
+        kp[page, t % ts] = (q[b, h] * 3.0).astype(np.float16)
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T)
+    for pps in (0, 8, 64):
+        out = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T,
+                                 pages_per_split=pps).cpu().numpy()
+        assert rel_err(out, ref) < RTOL
+
+
+def test_pa_decode_full_size_properties(gpu, oracle):
+    """C3 attention shape (B64 H16 D128 T8192 ts16, shuffled pages): exact
+    oracle parity on sampled (b, h) rows plus size-independent identities."""
+    import torch
+    import llm_capi
+    B, H, D, T, ts = 64, 16, 128, 8192, 16
+    nt = T // ts
+    num_pages = B * H * nt
+    g = torch.Generator(device="cuda").manual_seed(0)
+    kp = (torch.randn((num_pages, ts, D), generator=g, device="cuda") * D ** -0.25).half()
+    vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
+    q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
+    perm = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32)
+    pt = perm.reshape(B, H, nt).contiguous()
+    out = llm_capi.pa_decode(q, kp, vp, pt, T=T)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(0)
+    pt_h = pt.cpu().numpy()
+    for _ in range(6):
+        b, h = int(rng.integers(B)), int(rng.integers(H))
+        pages = pt_h[b, h]
+        kk = kp[torch.from_numpy(pages).long().cuda()].float().cpu().numpy()
+        vv = vp[torch.from_numpy(pages).long().cuda()].float().cpu().numpy()
+        sub_pt = np.arange(nt, dtype=np.int32).reshape(1, 1, nt)
+        ref = oracle.paged_attention(q[b:b + 1, h:h + 1].cpu().numpy(), kk, vv, sub_pt, T=T)
+        assert rel_err(out[b, h].cpu().numpy(), ref[0, 0]) < RTOL
+    # identity 1: constant V rows -> out == that row (sum p / (sum p + 1e-6))
+    c = torch.randn(D, device="cuda").half()
+    vconst = c.expand(num_pages, ts, D).contiguous()
+    o1 = llm_capi.pa_decode(q, kp, vconst, pt, T=T)
+    assert torch.allclose(o1, c.float().expand(B, H, D), rtol=1e-3, atol=1e-3)
+    # identity 2: K = 0 -> uniform softmax -> mean of V over the row's tokens
+    o2 = llm_capi.pa_decode(q, torch.zeros_like(kp), vp, pt, T=T)
+    mean = vp[pt.long()].float().mean(dim=(2, 3))  # [B][H][D]
+    assert rel_err(o2.cpu().numpy(), mean.cpu().numpy()) < RTOL
+
+
+def test_pa_decode_rejects_bad_shapes(gpu):
+    import ctypes
+    import torch
+    import llm_capi
+    lib = llm_capi.load()
+    kp = torch.zeros((4, 16, 64), dtype=torch.float16, device="cuda")
+    pt = torch.zeros((1, 2, 4), dtype=torch.int32, device="cuda")
+    view = llm_capi.kv_view(kp, kp, pt)
+    q = torch.zeros((1, 2, 64), device="cuda")
+    out = torch.zeros_like(q)
+    # H mismatch
+    rc = lib.pa_decode(ctypes.byref(view), llm_capi.ptr(q), llm_capi.ptr(out), None, None,
+                       1, 3, 64, 16, 1.0, 0, None, 0, llm_capi.stream_ptr())
+    assert rc == llm_capi.LLM_ERR_INVALID
+    # unsupported D
+    rc = lib.pa_decode(ctypes.byref(view), llm_capi.ptr(q), llm_capi.ptr(out), None, None,
+                       1, 2, 48, 16, 1.0, 0, None, 0, llm_capi.stream_ptr())
+    assert rc == llm_capi.LLM_ERR_INVALID
