@@ -1,0 +1,323 @@
+#!/usr/bin/env python3
+"""Decode throughput of the MI355X paged-attention INT8 decoder (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Workload (default, BASELINE config C3): INT8Decoder with 24 layers, 16 heads,
+head_dim 128 (hidden 2048, inter 8192, vocab 50257), 64 sequences per GPU,
+every sequence holding a KV context of 8192 tokens in shuffled 16-token pages
+(synthetic random fp16 K/V, random-init int8 weights — no checkpoints exist).
+A step = one full decode step of all 64 rows (embed, 24 x {LN, qkv GEMM, KV
+append, paged attention, o GEMM, LN, fc1, fc2}, tied LM head, argmax), replayed
+as a hipGraph; generation continues from step to step (the context grows).
+
+Multi-GPU: one process per GPU, sequences sharded by rank (weak scaling: 64 per
+GPU), no exchange inside a step; the final logits of every step are gathered to
+rank 0 over RCCL (the one collective of the design).  value = tokens/s of the
+whole job = 64 * N / t_step, t_step = max over ranks.
+
+Also reported (one JSON line on rank 0):
+  roofline     the paged-attention launch (the dominant kernel), timed live with
+               HIP events on the stream it runs on, against 8 TB/s HBM
+  cpu_baseline the oracle's restated INT8Decoder step on this host's cores
+               (bounded sample, see `sample`)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"
+sys.path.insert(0, str(PKG))
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # BASELINE.json configs[2]: the metric's config
+    "c3": dict(cls="INT8Decoder", L=24, H=16, D=128, V=50257, B=64, T=8192, ts=16,
+               workload="C3: INT8 decoder (MFMA i8 matmuls + fp16 paged attention), "
+                        "24-layer/16-head/d=128, 64 seqs/GPU, KV context 8192, page 16"),
+    # BASELINE.json configs[1]
+    "c2": dict(cls="CUDADecoder", L=12, H=12, D=64, V=50257, B=16, T=2048, ts=16,
+               workload="C2: fp16 paged decode, 12-layer/12-head/d=64, 16 seqs/GPU, "
+                        "KV context 2048, page 16"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_weights(cfg, seed):
+    rng = np.random.default_rng(seed)
+    L, hid, V = cfg["L"], cfg["H"] * cfg["D"], cfg["V"]
+    inter = 4 * hid
+    w = {"emb": rng.standard_normal((V, hid), dtype=np.float32).astype(np.float16).view(np.uint16)}
+    w["ln1_g"] = np.ones((L, hid), np.float32)
+    w["ln2_g"] = np.ones((L, hid), np.float32)
+    w["ln1_b"] = (0.1 * rng.standard_normal((L, hid), dtype=np.float32))
+    w["ln2_b"] = (0.1 * rng.standard_normal((L, hid), dtype=np.float32))
+    w["b1"] = (0.02 * rng.standard_normal((L, inter), dtype=np.float32))
+    w["b2"] = (0.02 * rng.standard_normal((L, hid), dtype=np.float32))
+    shapes = {"wqkv": (hid, 3 * hid), "wo": (hid, hid), "w1": (hid, inter), "w2": (inter, hid)}
+    if cfg["cls"] == "INT8Decoder":
+        for k, (K, N) in shapes.items():
+            w[k] = rng.integers(-127, 128, size=(L, K, N), dtype=np.int8)
+        scale = np.float32(0.02 * 3.0 / 127.0)
+        w["sw_qkv"] = np.full((L, 3 * hid), scale, np.float32)
+        w["sw_o"] = np.full((L, hid), scale, np.float32)
+        w["sw1"] = np.full((L, inter), scale, np.float32)
+        w["sw2"] = np.full((L, hid), scale, np.float32)
+    else:
+        for k, (K, N) in shapes.items():
+            w[k] = (0.02 * rng.standard_normal((L, K, N), dtype=np.float32)).astype(np.float16).view(np.uint16)
+    return w
+
+
+def step_bytes(cfg, T_mean, B):
+    """Algorithmic HBM bytes of one decode step: fp16 K+V of every
+    row/head/token, page-table entries, int8 weights + fp32 scales, q/out,
+    tied fp16 LM head.  Re-reads are not counted."""
+    L, H, D, V, ts = cfg["L"], cfg["H"], cfg["D"], cfg["V"], cfg["ts"]
+    hid, inter = H * D, 4 * H * D
+    nt = (T_mean + ts - 1) / ts
+    attn = 2 * B * H * T_mean * D * 2 + B * H * nt * 4 + 2 * B * hid * 4
+    wbytes = 1 if cfg["cls"] == "INT8Decoder" else 2
+    gemm = hid * (3 * hid + hid + 2 * inter) * wbytes + 4 * (3 * hid + hid + inter + hid)
+    return L * (attn + gemm) + V * hid * 2
+
+
+def attention_launch_bytes(cfg, T, B):
+    H, D, ts = cfg["H"], cfg["D"], cfg["ts"]
+    nt = (T + ts - 1) // ts
+    return 2 * B * H * T * D * 2 + B * H * nt * 4 + 2 * B * H * D * 4
+
+
+def time_attention(dec, cfg, B, T, max_seq, iters=20):
+    """Live HIP-event timing of the decoder's paged-attention launch (split +
+    merge, the same kernel instantiation and grid as inside the step graph) on
+    layer 0's pools, on torch's current stream."""
+    import torch
+    import llm_decoder
+    H, D = cfg["H"], cfg["D"]
+    q = torch.randn((B, H, D), device="cuda") * D ** -0.25
+    out = torch.empty((B, H, D), device="cuda")
+    ctx = torch.full((B,), T, dtype=torch.int32, device="cuda")
+    max_tiles = (max_seq + cfg["ts"] - 1) // cfg["ts"]
+    wsb = llm_decoder.workspace_bytes(B, H, D, max_tiles, 0)
+    ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        llm_decoder.paged_attention(dec.kv_handle, 0, q.data_ptr(), out.data_ptr(), 0,
+                                    ctx.data_ptr(), B, H, D, max_seq, 1.0, 0, 1.0,
+                                    ws.data_ptr(), wsb, st)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def cpu_baseline(cfg, budget_s=20.0):
+    """Oracle (restated INT8Decoder, C++/OpenMP) on this host: a bounded sample
+    of the same workload — SAMPLE_ROWS of the 64 rows through ONE layer at the
+    full KV context, plus the LM head for those rows; per-token time scaled to
+    all layers."""
+    from oracle.oracle import Oracle, OracleDecoder
+    o = Oracle(bench=True)
+    L, H, D, V, T = cfg["L"], cfg["H"], cfg["D"], cfg["V"], cfg["T"]
+    hid = H * D
+    rows = 16
+    one = dict(cfg, L=1)
+    w = make_weights(one, 99)
+    wd = {k: np.ascontiguousarray(v) for k, v in w.items()}
+    wd["emb"] = w["emb"].view(np.float16)
+    if cfg["cls"] != "INT8Decoder":
+        return None
+    wd["cfg"] = dict(L=1, H=H, D=D, hid=hid, inter=4 * hid, V=V, max_seq=T + 1)
+    dec = OracleDecoder(o, wd, rows)
+    rng = np.random.default_rng(0)
+    for which in (0, 1):  # fill the context: positive fp16 values in [0.125, 1)
+        kv = dec.kv(0, which)
+        kv[:, :, :T].view(np.uint16)[...] = rng.integers(0x3000, 0x3C00, kv[:, :, :T].shape,
+                                                          dtype=np.uint16)
+    toks = np.arange(rows, dtype=np.int32)
+    pos = np.full(rows, T, np.int32)
+    t0 = time.perf_counter()
+    n_layer = 0
+    t_layer = []
+    while True:
+        a = time.perf_counter()
+        dec.step(toks, pos, layers=1, lm_head=False)
+        t_layer.append(time.perf_counter() - a)
+        n_layer += 1
+        if time.perf_counter() - t0 > budget_s * 0.6 or n_layer >= 5:
+            break
+    a = time.perf_counter()
+    dec.step(toks, pos, layers=0, lm_head=True)
+    t_lm = time.perf_counter() - a
+    t_step = L * float(np.median(t_layer)) + t_lm
+    return {"value": rows / t_step, "unit": "tokens/s", "cores": o.num_threads(), "kind": "port",
+            "sample": f"{rows} of {cfg['B']} rows, 1 of {L} layers at KV context {T} "
+                      f"(median of {n_layer}) x {L} layers + LM head, oracle/liboracle_bench.so"}
+
+
+def load_traffic(cfg_name):
+    """HBM traffic of the attention launch from the committed rocprofv3 --pmc
+    summary (profiles/), if one exists for this config."""
+    p = ROOT / "profiles" / f"pmc_attention_{cfg_name}.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--seed", type=int, default=1234)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import llm_decoder  # noqa: F401  (fails loudly if the HIP build is missing)
+
+    cfg = CONFIGS[args.config]
+    B, T = cfg["B"], cfg["T"]
+    hid = cfg["H"] * cfg["D"]
+    max_seq = T + args.warmup + args.steps + 8
+    cls = getattr(llm_decoder, cfg["cls"])
+    t0 = time.time()
+    dec = cls(cfg["L"], cfg["H"], cfg["D"], hid, cfg["V"], max_seq, max_batch=B,
+              page_size=cfg["ts"])
+    w = make_weights(cfg, args.seed)
+    dec.set_weights(w)
+    del w
+    dec.begin_synthetic(B, T, args.seed + rank, True)
+    log(f"[rank {rank}] setup {time.time() - t0:.1f}s")
+
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    logits = [torch.empty((B, cfg["V"]), device="cuda") for _ in range(2)]
+    gather_bufs = ([[torch.empty_like(logits[0]) for _ in range(world)] for _ in range(2)]
+                   if world > 1 and rank == 0 else [None, None])
+    works = [None, None]
+    tokens = np.random.default_rng(args.seed + rank).integers(0, cfg["V"], B).astype(np.int32)
+
+    def one_step(i, first):
+        slot = i % 2
+        if works[slot] is not None:
+            works[slot].wait()
+        dec.step(list(map(int, tokens)) if first else None,
+                 logits_ptr=logits[slot].data_ptr() if world > 1 else 0,
+                 stream=sp, want_next=False)
+        if world > 1:
+            works[slot] = dist.gather(logits[slot], gather_bufs[slot] if rank == 0 else None,
+                                      dst=0, async_op=True)
+
+    for i in range(args.warmup):
+        one_step(i, i == 0)
+    torch.cuda.synchronize()
+    if world > 1:
+        for wk in works:
+            if wk is not None:
+                wk.wait()
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        one_step(i, args.warmup == 0 and i == 0)
+    for wk in works:
+        if wk is not None:
+            wk.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    t_step = elapsed / args.steps
+    T_mean = T + args.warmup + args.steps / 2.0
+    value = B * world / t_step
+
+    # roofline of the dominant kernel (paged attention), timed live
+    T_now = dec.context_len(0)
+    t_attn = time_attention(dec, cfg, B, T_now, max_seq)
+    attn_b = attention_launch_bytes(cfg, T_now, B)
+    achieved = attn_b / t_attn / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": load_traffic(args.config),
+            "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}> + pa_merge_kernel",
+            "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
+    step_b = step_bytes(cfg, T_mean, B)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(cfg, args.cpu_budget)
+        except Exception as ex:  # the baseline never blocks the GPU number
+            log(f"cpu baseline failed: {ex!r}")
+    if rank == 0:
+        res = {
+            "metric": "decode tokens/sec at batch=64 seq_len=8192; % HBM-roofline (1/2/4/8 GPU)"
+            if args.config == "c3" else f"decode tokens/sec ({args.config})",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8 GEMM (i32 acc) + fp16 KV attention (fp32 acc)"
+            if cfg["cls"] == "INT8Decoder" else "fp16 GEMM + fp16 KV attention (fp32 acc)",
+            "data": "synthetic (random-init weights, random fp16 KV context, shuffled pages)",
+            "config": {"workload": cfg["workload"], "global_batch": B * world,
+                       "batch_per_gpu": B, "seq_len": T, "page_size": cfg["ts"],
+                       "parallelism": f"batch-sharded x{world} (RCCL logits gather to rank 0)"},
+            "hbm_roofline_frac_step": round(step_b / t_step / 1e9 / HBM_PEAK_GBPS, 4),
+            "step_bytes": int(step_b),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

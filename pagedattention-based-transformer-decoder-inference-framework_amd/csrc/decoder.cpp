@@ -1,0 +1,684 @@
+// Decoder runtime (host side, compiled as HIP): CUDADecoder / INT8Decoder
+// (decoder/cuda_decoder.{hpp,cu}, decoder/int8_decoder.{hpp,cpp}) re-designed
+// for batched incremental decode on one MI355X.
+//
+// One decode step for all rows (reference layer order of
+// DecoderBlock<T>::forward, decoder/decoder_block.hpp:41-62 — no residuals —
+// plus the BUILD DECISION projections):
+//   embed -> per layer { LN1+quant -> qkv GEMM -> KV append -> paged attention
+//   -> quant -> o GEMM -> LN2+quant -> fc1 GEMM (+b1, ReLU) -> quant -> fc2 GEMM
+//   (+b2) } -> LM head (tied fp16 embedding) -> argmax -> advance positions.
+// The reference re-embeds and recomputes the whole prefix every step
+// (decoder/cuda_decoder.cu:52-57) and runs B = 1; here the KV cache is
+// appended in place and the step is O(T) per row.
+//
+// The device part of a step is captured once per batch size into a hipGraph
+// and replayed; per-step state (positions, context lengths, tokens) lives in
+// device memory, so replays need no re-capture.  Only page allocation (a new
+// page every page_size tokens, copy-on-write of forked pages) happens on the
+// host between replays and is pushed with kv_cache_sync().
+#include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kv_cache_impl.hpp"
+#include "pa_decode.hpp"
+#include "row_ops.hpp"
+
+using namespace llm;
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  int alloc(size_t count) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    n = count;
+    if (count == 0) return LLM_OK;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(LLM_ERR_OOM, "decoder: device allocation of " + std::to_string(count * sizeof(T)) +
+                                   " bytes failed");
+    }
+    return LLM_OK;
+  }
+};
+
+#define RET_IF(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
+
+}  // namespace
+
+struct llm_decoder {
+  llm_decoder_config cfg{};
+  int L = 0, H = 0, D = 0, hid = 0, inter = 0, V = 0, TS = 0, max_tiles = 0, maxB = 0;
+  int wdtype = LLM_I8;
+  int pps = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+
+  // weights
+  DevBuf<uint16_t> emb;
+  DevBuf<float> ln1_g, ln1_b, ln2_g, ln2_b, b1, b2, sw_qkv, sw_o, sw1, sw2;
+  DevBuf<uint8_t> wqkv, wo, w1, w2;  // packed, L consecutive blocks
+  size_t sz_qkv = 0, sz_o = 0, sz_1 = 0, sz_2 = 0;
+  bool weights_ready = false;
+
+  // KV
+  kv_cache* kv = nullptr;
+
+  // activations / state
+  DevBuf<float> x, qkv, o, h1, logits, sa;
+  DevBuf<int8_t> qa;
+  DevBuf<uint16_t> a16;
+  DevBuf<int32_t> tokens, pos, ctx;
+  DevBuf<uint8_t> attn_ws;
+  size_t attn_ws_bytes = 0;
+
+  int batch = 0;
+  std::vector<int> h_pos;  // host mirror of the next position of each row
+
+  hipGraphExec_t graph = nullptr;
+  int graph_batch = -1;
+
+  ~llm_decoder() {
+    if (graph) (void)hipGraphExecDestroy(graph);
+    if (kv) kv_cache_destroy(kv);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  int layer_forward_int8(int l, hipStream_t st);
+  int layer_forward_f16(int l, hipStream_t st);
+  int enqueue_step(hipStream_t st);
+  int run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host, hipStream_t st);
+};
+
+static int check_cfg(const llm_decoder_config& c) {
+  LLM_REQUIRE(c.num_layers > 0 && c.num_heads > 0 && c.head_dim > 0 && c.vocab_size > 0 &&
+                  c.max_seq_len > 0,
+              "decoder: num_layers/num_heads/head_dim/vocab_size/max_seq_len must be positive");
+  LLM_REQUIRE(c.hidden_dim == c.num_heads * c.head_dim,
+              "decoder: hidden_dim must equal num_heads * head_dim");
+  LLM_REQUIRE(c.weight_dtype == LLM_I8 || c.weight_dtype == LLM_F16, "decoder: weight_dtype");
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder** out) {
+  LLM_REQUIRE(cfg_in && out, "llm_decoder_create: NULL");
+  llm_decoder_config c = *cfg_in;
+  if (c.inter_dim <= 0) c.inter_dim = 4 * c.hidden_dim;
+  if (c.page_size <= 0) c.page_size = 16;
+  if (c.max_batch <= 0) c.max_batch = 1;
+  if (c.attn_scale == 0.f) c.attn_scale = 1.f;
+  RET_IF(check_cfg(c));
+  const int kstep = c.weight_dtype == LLM_I8 ? 64 : 32;
+  LLM_REQUIRE(c.hidden_dim % kstep == 0 && c.inter_dim % kstep == 0,
+              "decoder: hidden_dim and inter_dim must be multiples of 64 (int8) / 32 (fp16)");
+  std::unique_ptr<llm_decoder> d(new llm_decoder());
+  d->cfg = c;
+  d->L = c.num_layers; d->H = c.num_heads; d->D = c.head_dim; d->hid = c.hidden_dim;
+  d->inter = c.inter_dim; d->V = c.vocab_size; d->TS = c.page_size;
+  d->max_tiles = (c.max_seq_len + c.page_size - 1) / c.page_size;
+  d->maxB = c.max_batch;
+  d->wdtype = c.weight_dtype;
+  LLM_HIP_RET(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+  long long pages = c.num_pages > 0 ? c.num_pages
+                                     : (long long)d->maxB * d->L * d->H * d->max_tiles;
+  RET_IF(kv_cache_create(d->L, d->maxB, d->H, d->D, d->TS, d->max_tiles, pages, &d->kv));
+  const int B = d->maxB, hid = d->hid, inter = d->inter;
+  RET_IF(d->x.alloc((size_t)B * hid));
+  RET_IF(d->qkv.alloc((size_t)B * 3 * hid));
+  RET_IF(d->o.alloc((size_t)B * hid));
+  RET_IF(d->h1.alloc((size_t)B * inter));
+  RET_IF(d->logits.alloc((size_t)B * d->V));
+  RET_IF(d->sa.alloc((size_t)B));
+  RET_IF(d->qa.alloc((size_t)B * std::max(hid, inter)));
+  if (d->wdtype == LLM_F16) RET_IF(d->a16.alloc((size_t)B * std::max(hid, inter)));
+  RET_IF(d->tokens.alloc((size_t)B));
+  RET_IF(d->pos.alloc((size_t)B));
+  RET_IF(d->ctx.alloc((size_t)B));
+  d->pps = pa_pages_per_split(B, d->H, c.max_seq_len, d->TS, d->max_tiles);
+  d->attn_ws_bytes = pa_decode_workspace_bytes(B, d->H, d->D, d->max_tiles, d->pps);
+  RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
+  d->h_pos.assign(B, 0);
+  *out = d.release();
+  return LLM_OK;
+}
+
+extern "C" void llm_decoder_destroy(llm_decoder* d) {
+  if (!d) return;
+  if (d->stream) (void)hipStreamSynchronize(d->stream);
+  delete d;
+}
+
+extern "C" kv_cache* llm_decoder_kv(llm_decoder* d) { return d ? d->kv : nullptr; }
+
+// ---------------------------------------------------------------------------
+// weights
+// ---------------------------------------------------------------------------
+template <typename T>
+static int upload(DevBuf<T>& dst, const T* src, size_t n, const char* what) {
+  LLM_REQUIRE(src != nullptr, std::string("decoder weights: ") + what + " is NULL");
+  RET_IF(dst.alloc(n));
+  LLM_HIP_RET(hipMemcpy(dst.p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return LLM_OK;
+}
+
+// Upload L row-major [K][N] matrices and pack each into MFMA fragment order.
+static int upload_packed(DevBuf<uint8_t>& dst, size_t& per_layer, const void* src, int L, int K,
+                         int N, int dtype, const char* what) {
+  LLM_REQUIRE(src != nullptr, std::string("decoder weights: ") + what + " is NULL");
+  const size_t esz = dtype == LLM_I8 ? 1 : 2;
+  per_layer = gemm_packed_bytes(dtype, K, N);
+  RET_IF(dst.alloc(per_layer * L));
+  void* tmp = nullptr;
+  LLM_HIP_RET(hipMalloc(&tmp, (size_t)K * N * esz));
+  int rc = LLM_OK;
+  for (int l = 0; l < L && rc == LLM_OK; ++l) {
+    const char* s = static_cast<const char*>(src) + (size_t)l * K * N * esz;
+    if (hipMemcpy(tmp, s, (size_t)K * N * esz, hipMemcpyHostToDevice) != hipSuccess) {
+      rc = fail(LLM_ERR_HIP, "decoder weights: upload failed");
+      break;
+    }
+    rc = gemm_pack_weights(dtype, tmp, dst.p + per_layer * l, K, N, nullptr);
+  }
+  (void)hipDeviceSynchronize();
+  (void)hipFree(tmp);
+  return rc;
+}
+
+static int upload_common(llm_decoder* d, const uint16_t* emb, const float* ln1_g,
+                         const float* ln1_b, const float* ln2_g, const float* ln2_b) {
+  const size_t Lh = (size_t)d->L * d->hid;
+  RET_IF(upload(d->emb, emb, (size_t)d->V * d->hid, "emb"));
+  RET_IF(upload(d->ln1_g, ln1_g, Lh, "ln1_g"));
+  RET_IF(upload(d->ln1_b, ln1_b, Lh, "ln1_b"));
+  RET_IF(upload(d->ln2_g, ln2_g, Lh, "ln2_g"));
+  RET_IF(upload(d->ln2_b, ln2_b, Lh, "ln2_b"));
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_set_int8_weights(llm_decoder* d, const llm_int8_weights* w) {
+  LLM_REQUIRE(d && w, "llm_decoder_set_int8_weights: NULL");
+  LLM_REQUIRE(d->wdtype == LLM_I8, "llm_decoder_set_int8_weights: decoder is not INT8");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  const int L = d->L, hid = d->hid, inter = d->inter;
+  RET_IF(upload_common(d, w->emb, w->ln1_g, w->ln1_b, w->ln2_g, w->ln2_b));
+  RET_IF(upload_packed(d->wqkv, d->sz_qkv, w->wqkv, L, hid, 3 * hid, LLM_I8, "wqkv"));
+  RET_IF(upload_packed(d->wo, d->sz_o, w->wo, L, hid, hid, LLM_I8, "wo"));
+  RET_IF(upload_packed(d->w1, d->sz_1, w->w1, L, hid, inter, LLM_I8, "w1"));
+  RET_IF(upload_packed(d->w2, d->sz_2, w->w2, L, inter, hid, LLM_I8, "w2"));
+  RET_IF(upload(d->sw_qkv, w->sw_qkv, (size_t)L * 3 * hid, "sw_qkv"));
+  RET_IF(upload(d->sw_o, w->sw_o, (size_t)L * hid, "sw_o"));
+  RET_IF(upload(d->sw1, w->sw1, (size_t)L * inter, "sw1"));
+  RET_IF(upload(d->sw2, w->sw2, (size_t)L * hid, "sw2"));
+  RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
+  RET_IF(upload(d->b2, w->b2, (size_t)L * hid, "b2"));
+  d->weights_ready = true;
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights* w) {
+  LLM_REQUIRE(d && w, "llm_decoder_set_f16_weights: NULL");
+  LLM_REQUIRE(d->wdtype == LLM_F16, "llm_decoder_set_f16_weights: decoder is not FP16");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  const int L = d->L, hid = d->hid, inter = d->inter;
+  RET_IF(upload_common(d, w->emb, w->ln1_g, w->ln1_b, w->ln2_g, w->ln2_b));
+  RET_IF(upload_packed(d->wqkv, d->sz_qkv, w->wqkv, L, hid, 3 * hid, LLM_F16, "wqkv"));
+  RET_IF(upload_packed(d->wo, d->sz_o, w->wo, L, hid, hid, LLM_F16, "wo"));
+  RET_IF(upload_packed(d->w1, d->sz_1, w->w1, L, hid, inter, LLM_F16, "w1"));
+  RET_IF(upload_packed(d->w2, d->sz_2, w->w2, L, inter, hid, LLM_F16, "w2"));
+  RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
+  RET_IF(upload(d->b2, w->b2, (size_t)L * hid, "b2"));
+  d->weights_ready = true;
+  return LLM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// step
+// ---------------------------------------------------------------------------
+int llm_decoder::layer_forward_int8(int l, hipStream_t st) {
+  const int B = batch;
+  const size_t lh = (size_t)l * hid;
+  const int qa_ld = std::max(hid, inter);
+  (void)qa_ld;
+  // LN1 + quant (rows of `hid` int8 at stride hid)
+  LLM_HIP_RET(launch_layernorm_quant(x.p, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
+                                     qa.p, sa.p, st));
+  RET_IF(i8_gemm(qa.p, hid, wqkv.p + sz_qkv * l, nullptr, qkv.p, B, 3 * hid, hid, sa.p,
+                 sw_qkv.p + (size_t)l * 3 * hid, nullptr, LLM_ACT_NONE, st));
+  pa_kv_view view;
+  RET_IF(kv_cache_view(kv, l, &view));
+  LLM_HIP_RET(launch_kv_append(qkv.p, B, H, D, pos.p, view.page_table, view.num_beams,
+                               view.max_tiles, TS, view.num_pages, kv_cache_k_pool(kv),
+                               kv_cache_v_pool(kv), st));
+  RET_IF(pa_decode_internal(&view, qkv.p, 3 * hid, o.p, nullptr, ctx.p, B, H, D,
+                            cfg.max_seq_len, cfg.attn_scale, pps, attn_ws.p, attn_ws_bytes, st));
+  LLM_HIP_RET(launch_quantize_rows(o.p, B, hid, qa.p, sa.p, st));
+  RET_IF(i8_gemm(qa.p, hid, wo.p + sz_o * l, nullptr, x.p, B, hid, hid, sa.p, sw_o.p + lh,
+                 nullptr, LLM_ACT_NONE, st));
+  LLM_HIP_RET(launch_layernorm_quant(x.p, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
+                                     qa.p, sa.p, st));
+  RET_IF(i8_gemm(qa.p, hid, w1.p + sz_1 * l, nullptr, h1.p, B, inter, hid, sa.p,
+                 sw1.p + (size_t)l * inter, b1.p + (size_t)l * inter, LLM_ACT_RELU, st));
+  LLM_HIP_RET(launch_quantize_rows(h1.p, B, inter, qa.p, sa.p, st));
+  RET_IF(i8_gemm(qa.p, inter, w2.p + sz_2 * l, nullptr, x.p, B, hid, inter, sa.p, sw2.p + lh,
+                 b2.p + lh, LLM_ACT_NONE, st));
+  return LLM_OK;
+}
+
+int llm_decoder::layer_forward_f16(int l, hipStream_t st) {
+  const int B = batch;
+  const size_t lh = (size_t)l * hid;
+  LLM_HIP_RET(launch_layernorm_f16(x.p, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, a16.p, st));
+  RET_IF(f16_gemm(a16.p, hid, wqkv.p + sz_qkv * l, qkv.p, B, 3 * hid, hid, nullptr, LLM_ACT_NONE,
+                  st));
+  pa_kv_view view;
+  RET_IF(kv_cache_view(kv, l, &view));
+  LLM_HIP_RET(launch_kv_append(qkv.p, B, H, D, pos.p, view.page_table, view.num_beams,
+                               view.max_tiles, TS, view.num_pages, kv_cache_k_pool(kv),
+                               kv_cache_v_pool(kv), st));
+  RET_IF(pa_decode_internal(&view, qkv.p, 3 * hid, o.p, nullptr, ctx.p, B, H, D,
+                            cfg.max_seq_len, cfg.attn_scale, pps, attn_ws.p, attn_ws_bytes, st));
+  LLM_HIP_RET(launch_to_f16(o.p, (size_t)B * hid, a16.p, st));
+  RET_IF(f16_gemm(a16.p, hid, wo.p + sz_o * l, x.p, B, hid, hid, nullptr, LLM_ACT_NONE, st));
+  LLM_HIP_RET(launch_layernorm_f16(x.p, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, a16.p, st));
+  RET_IF(f16_gemm(a16.p, hid, w1.p + sz_1 * l, h1.p, B, inter, hid, b1.p + (size_t)l * inter,
+                  LLM_ACT_RELU, st));
+  LLM_HIP_RET(launch_to_f16(h1.p, (size_t)B * inter, a16.p, st));
+  RET_IF(f16_gemm(a16.p, inter, w2.p + sz_2 * l, x.p, B, hid, inter, b2.p + lh, LLM_ACT_NONE, st));
+  return LLM_OK;
+}
+
+int llm_decoder::enqueue_step(hipStream_t st) {
+  LLM_HIP_RET(launch_embed(emb.p, tokens.p, batch, hid, V, x.p, st));
+  for (int l = 0; l < L; ++l) RET_IF(wdtype == LLM_I8 ? layer_forward_int8(l, st) : layer_forward_f16(l, st));
+  RET_IF(lm_head(x.p, emb.p, logits.p, batch, V, hid, st));
+  LLM_HIP_RET(launch_argmax(logits.p, batch, V, tokens.p, nullptr, 0, st));  // next tokens in place
+  LLM_HIP_RET(launch_advance(pos.p, ctx.p, batch, st));
+  return LLM_OK;
+}
+
+int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host,
+                          hipStream_t st) {
+  LLM_REQUIRE(weights_ready, "decoder: weights not loaded");
+  LLM_REQUIRE(batch > 0, "decoder: no active rows (call generate / begin first)");
+  KvCache* k = kv_impl(kv);
+  {
+    std::lock_guard<std::mutex> g(k->mu);
+    for (int b = 0; b < batch; ++b) {
+      LLM_REQUIRE(h_pos[b] < cfg.max_seq_len, "decoder: row reached max_seq_len");
+      RET_IF(k->prepare_append(b, h_pos[b]));
+    }
+    RET_IF(k->sync(st));
+  }
+  if (tokens_host) {
+    for (int b = 0; b < batch; ++b)
+      LLM_REQUIRE(tokens_host[b] >= 0 && tokens_host[b] < V, "decoder: token id out of range");
+    LLM_HIP_RET(hipMemcpyAsync(tokens.p, tokens_host, sizeof(int32_t) * batch,
+                               hipMemcpyHostToDevice, st));
+  }
+  if (graph_batch != batch) {
+    if (graph) { (void)hipGraphExecDestroy(graph); graph = nullptr; }
+    hipGraph_t g;
+    LLM_HIP_RET(hipStreamSynchronize(st));
+    LLM_HIP_RET(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_step(stream);
+    hipError_t e = hipStreamEndCapture(stream, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(e));
+    graph_batch = batch;
+  }
+  LLM_HIP_RET(hipGraphLaunch(graph, st));
+  for (int b = 0; b < batch; ++b) h_pos[b] += 1;
+  if (logits_dev)
+    LLM_HIP_RET(hipMemcpyAsync(logits_dev, logits.p, sizeof(float) * batch * V,
+                               hipMemcpyDeviceToDevice, st));
+  if (next_host) {
+    LLM_HIP_RET(hipMemcpyAsync(next_host, tokens.p, sizeof(int32_t) * batch,
+                               hipMemcpyDeviceToHost, st));
+    LLM_HIP_RET(hipStreamSynchronize(st));
+  }
+  return LLM_OK;
+}
+
+static int reset_rows(llm_decoder* d, int batch, int start_pos) {
+  LLM_REQUIRE(batch > 0 && batch <= d->maxB, "decoder: batch must be in [1, max_batch]");
+  RET_IF(kv_cache_clear(d->kv));
+  d->batch = batch;
+  d->h_pos.assign(d->maxB, 0);
+  for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
+  std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
+  LLM_HIP_RET(hipMemcpy(d->pos.p, pos.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
+  LLM_HIP_RET(hipMemcpy(d->ctx.p, ctx.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
+  LLM_HIP_RET(hipMemcpy(d->tokens.p, tok.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
+  LLM_HIP_RET(hipDeviceSynchronize());
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_begin_synthetic(llm_decoder* d, int batch, int context_len,
+                                           uint64_t seed, int shuffle) {
+  LLM_REQUIRE(d, "llm_decoder_begin_synthetic: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_REQUIRE(context_len >= 0 && context_len < d->cfg.max_seq_len,
+              "llm_decoder_begin_synthetic: context_len must be in [0, max_seq_len)");
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  RET_IF(reset_rows(d, batch, context_len));
+  KvCache* k = kv_impl(d->kv);
+  {
+    std::lock_guard<std::mutex> gk(k->mu);
+    if (shuffle) {  // non-contiguous page gather (shuffled page pool, seed 7)
+      std::mt19937_64 rng(seed ^ 7);
+      std::shuffle(k->free_list.begin(), k->free_list.end(), rng);
+    }
+  }
+  for (int b = 0; b < batch; ++b) RET_IF(kv_cache_reserve(d->kv, b, context_len));
+  RET_IF(kv_cache_sync(d->kv, d->stream));
+  // seeded random fp16 K/V over the whole pools (K scaled so q.k ~ O(1))
+  const size_t n = (size_t)k->num_pages * k->page_elems;
+  LLM_HIP_RET(launch_fill_random_f16(k->k_pool, n, seed * 2 + 1, 0.05f, d->stream));
+  LLM_HIP_RET(launch_fill_random_f16(k->v_pool, n, seed * 2 + 2, 1.0f, d->stream));
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
+                                int32_t* next_host, void* stream) {
+  LLM_REQUIRE(d, "llm_decoder_step: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  hipStream_t st = stream ? as_stream(stream) : d->stream;
+  return d->run_step(tokens, logits_dev, next_host, st);
+}
+
+extern "C" int llm_decoder_sync(llm_decoder* d) {
+  LLM_REQUIRE(d, "llm_decoder_sync: NULL");
+  LLM_HIP_RET(hipDeviceSynchronize());
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_context_len(const llm_decoder* d, int row) {
+  if (!d || row < 0 || row >= d->batch) return -1;
+  return d->h_pos[row];
+}
+
+extern "C" int llm_decoder_generate(llm_decoder* d, const int32_t* prompts,
+                                    const int32_t* prompt_lens, int prompt_stride, int batch,
+                                    int max_gen_len, float temperature, int32_t* out) {
+  LLM_REQUIRE(d && prompts && prompt_lens && out, "llm_decoder_generate: NULL");
+  LLM_REQUIRE(max_gen_len >= 0, "llm_decoder_generate: max_gen_len < 0");
+  (void)temperature;  // greedy argmax is invariant to temperature > 0 (cuda_decoder.cu:7-14)
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_REQUIRE(batch >= 1 && batch <= d->maxB, "llm_decoder_generate: batch out of range");
+  int max_len = 0;
+  for (int b = 0; b < batch; ++b) {
+    LLM_REQUIRE(prompt_lens[b] >= 1 && prompt_lens[b] <= prompt_stride,
+                "llm_decoder_generate: every prompt needs >= 1 token");
+    for (int i = 0; i < prompt_lens[b]; ++i) {
+      const int t = prompts[(size_t)b * prompt_stride + i];
+      LLM_REQUIRE(t >= 0 && t < d->V, "llm_decoder_generate: token id out of range");
+    }
+    max_len = std::max(max_len, prompt_lens[b]);
+  }
+  if (max_gen_len == 0) return LLM_OK;
+  LLM_REQUIRE(max_len + max_gen_len - 1 <= d->cfg.max_seq_len,
+              "llm_decoder_generate: prompt + max_gen_len exceeds max_seq_len");
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  RET_IF(reset_rows(d, batch, 0));
+  const int steps = max_len + max_gen_len - 1;
+  std::vector<int32_t> tok(batch), next(batch);
+  for (int s = 0; s < steps; ++s) {
+    for (int b = 0; b < batch; ++b)
+      tok[b] = s < prompt_lens[b] ? prompts[(size_t)b * prompt_stride + s] : next[b];
+    RET_IF(d->run_step(tok.data(), nullptr, next.data(), d->stream));
+    for (int b = 0; b < batch; ++b) {
+      const int gi = s - (prompt_lens[b] - 1);
+      if (gi >= 0 && gi < max_gen_len) out[(size_t)b * max_gen_len + gi] = next[b];
+    }
+  }
+  return LLM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// weight files (weights/README.md:26-38; raw little-endian .bin)
+// ---------------------------------------------------------------------------
+static int read_file(const std::string& path, std::vector<char>& buf, size_t expect) {
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  if (!f) return fail(LLM_ERR_IO, "cannot open weight file: " + path);  // decoder_block.hpp:13-15
+  const size_t size = (size_t)f.tellg();
+  if (expect && size != expect)
+    return fail(LLM_ERR_IO, path + ": expected " + std::to_string(expect) + " bytes, found " +
+                                std::to_string(size));
+  buf.resize(size);
+  f.seekg(0);
+  f.read(buf.data(), size);
+  if (!f) return fail(LLM_ERR_IO, "failed to read from file: " + path);
+  return LLM_OK;
+}
+
+static int write_file(const std::string& path, const void* p, size_t n) {
+  std::ofstream f(path, std::ios::binary);
+  if (!f) return fail(LLM_ERR_IO, "cannot create " + path);
+  f.write(static_cast<const char*>(p), n);
+  if (!f) return fail(LLM_ERR_IO, "write failed: " + path);
+  return LLM_OK;
+}
+
+static uint16_t f32_to_f16_bits(float f) {
+  const _Float16 h = (_Float16)f;
+  uint16_t u;
+  std::memcpy(&u, &h, 2);
+  return u;
+}
+
+// fp32 directory (CUDADecoder::load_weights): embedding.bin [V][hid];
+// layer_i/{ln1.bin, ln2.bin} gamma+beta; attn_wq/wk/wv/wo.bin [hid][hid];
+// mlp_fc1.bin [hid][inter]; mlp_fc2.bin [inter][hid]; mlp_biases.bin [inter+hid].
+struct Fp32Model {
+  std::vector<float> emb, ln1, ln2, wqkv, wo, w1, w2, b1, b2;  // ln: [L][2][hid]
+};
+
+static int load_fp32_dir(const std::string& dir, int L, int hid, int inter, int V, Fp32Model& m) {
+  std::vector<char> buf;
+  auto rd = [&](const std::string& p, size_t n, float* dst) -> int {
+    RET_IF(read_file(p, buf, n * 4));
+    std::memcpy(dst, buf.data(), n * 4);
+    return LLM_OK;
+  };
+  m.emb.resize((size_t)V * hid);
+  RET_IF(rd(dir + "/embedding.bin", m.emb.size(), m.emb.data()));
+  m.ln1.resize((size_t)L * 2 * hid); m.ln2.resize((size_t)L * 2 * hid);
+  m.wqkv.resize((size_t)L * hid * 3 * hid); m.wo.resize((size_t)L * hid * hid);
+  m.w1.resize((size_t)L * hid * inter); m.w2.resize((size_t)L * inter * hid);
+  m.b1.resize((size_t)L * inter); m.b2.resize((size_t)L * hid);
+  std::vector<float> tmp((size_t)hid * hid), bias(inter + hid);
+  for (int l = 0; l < L; ++l) {
+    const std::string p = dir + "/layer_" + std::to_string(l);
+    RET_IF(rd(p + "/ln1.bin", 2 * hid, m.ln1.data() + (size_t)l * 2 * hid));
+    RET_IF(rd(p + "/ln2.bin", 2 * hid, m.ln2.data() + (size_t)l * 2 * hid));
+    const char* names[3] = {"/attn_wq.bin", "/attn_wk.bin", "/attn_wv.bin"};
+    for (int j = 0; j < 3; ++j) {  // fuse q|k|v column blocks: Wqkv[k][j*hid + n]
+      RET_IF(rd(p + names[j], (size_t)hid * hid, tmp.data()));
+      float* dst = m.wqkv.data() + (size_t)l * hid * 3 * hid;
+      for (int k = 0; k < hid; ++k)
+        std::memcpy(dst + (size_t)k * 3 * hid + (size_t)j * hid, tmp.data() + (size_t)k * hid,
+                    hid * 4);
+    }
+    RET_IF(rd(p + "/attn_wo.bin", (size_t)hid * hid, m.wo.data() + (size_t)l * hid * hid));
+    RET_IF(rd(p + "/mlp_fc1.bin", (size_t)hid * inter, m.w1.data() + (size_t)l * hid * inter));
+    RET_IF(rd(p + "/mlp_fc2.bin", (size_t)inter * hid, m.w2.data() + (size_t)l * inter * hid));
+    RET_IF(rd(p + "/mlp_biases.bin", (size_t)inter + hid, bias.data()));
+    std::memcpy(m.b1.data() + (size_t)l * inter, bias.data(), (size_t)inter * 4);
+    std::memcpy(m.b2.data() + (size_t)l * hid, bias.data() + inter, (size_t)hid * 4);
+  }
+  return LLM_OK;
+}
+
+static void split_ln(const std::vector<float>& ln, int L, int hid, std::vector<float>& g,
+                     std::vector<float>& b) {
+  g.resize((size_t)L * hid);
+  b.resize((size_t)L * hid);
+  for (int l = 0; l < L; ++l) {
+    std::memcpy(g.data() + (size_t)l * hid, ln.data() + (size_t)l * 2 * hid, hid * 4);
+    std::memcpy(b.data() + (size_t)l * hid, ln.data() + (size_t)l * 2 * hid + hid, hid * 4);
+  }
+}
+
+// Per-output-column int8 quantisation (int8_quant.cpp semantics, one scale per column).
+static void quantize_cols(const float* w, int K, int N, int8_t* q, float* inv) {
+  for (int n = 0; n < N; ++n) {
+    float mn = w[n], mx = w[n];
+    for (int k = 1; k < K; ++k) {
+      mn = std::min(mn, w[(size_t)k * N + n]);
+      mx = std::max(mx, w[(size_t)k * N + n]);
+    }
+    const float absmax = std::max(std::fabs(mn), std::fabs(mx));
+    const float scale = 127.f / (absmax + 1e-6f);
+    for (int k = 0; k < K; ++k) {
+      int v = (int)std::round(w[(size_t)k * N + n] * scale);
+      v = std::max(-128, std::min(127, v));
+      q[(size_t)k * N + n] = (int8_t)v;
+    }
+    inv[n] = 1.0f / scale;
+  }
+}
+
+extern "C" int llm_decoder_load_weights(llm_decoder* d, const char* dir) {
+  LLM_REQUIRE(d && dir, "llm_decoder_load_weights: NULL");
+  const int L = d->L, hid = d->hid, inter = d->inter, V = d->V;
+  Fp32Model m;
+  RET_IF(load_fp32_dir(dir, L, hid, inter, V, m));
+  std::vector<float> g1, be1, g2, be2;
+  split_ln(m.ln1, L, hid, g1, be1);
+  split_ln(m.ln2, L, hid, g2, be2);
+  std::vector<uint16_t> emb(m.emb.size());
+  for (size_t i = 0; i < emb.size(); ++i) emb[i] = f32_to_f16_bits(m.emb[i]);
+  if (d->wdtype == LLM_F16) {
+    auto cvt = [](const std::vector<float>& s) {
+      std::vector<uint16_t> o(s.size());
+      for (size_t i = 0; i < s.size(); ++i) o[i] = f32_to_f16_bits(s[i]);
+      return o;
+    };
+    auto qkv = cvt(m.wqkv), wo = cvt(m.wo), w1 = cvt(m.w1), w2 = cvt(m.w2);
+    llm_f16_weights w{emb.data(), g1.data(), be1.data(), g2.data(), be2.data(), qkv.data(),
+                      wo.data(), w1.data(), w2.data(), m.b1.data(), m.b2.data()};
+    return llm_decoder_set_f16_weights(d, &w);
+  }
+  // INT8 decoder given fp32 weights: quantise on load
+  std::vector<int8_t> qqkv(m.wqkv.size()), qo(m.wo.size()), q1(m.w1.size()), q2(m.w2.size());
+  std::vector<float> sqkv((size_t)L * 3 * hid), so((size_t)L * hid), s1((size_t)L * inter),
+      s2((size_t)L * hid);
+  for (int l = 0; l < L; ++l) {
+    quantize_cols(m.wqkv.data() + (size_t)l * hid * 3 * hid, hid, 3 * hid,
+                  qqkv.data() + (size_t)l * hid * 3 * hid, sqkv.data() + (size_t)l * 3 * hid);
+    quantize_cols(m.wo.data() + (size_t)l * hid * hid, hid, hid, qo.data() + (size_t)l * hid * hid,
+                  so.data() + (size_t)l * hid);
+    quantize_cols(m.w1.data() + (size_t)l * hid * inter, hid, inter,
+                  q1.data() + (size_t)l * hid * inter, s1.data() + (size_t)l * inter);
+    quantize_cols(m.w2.data() + (size_t)l * inter * hid, inter, hid,
+                  q2.data() + (size_t)l * inter * hid, s2.data() + (size_t)l * hid);
+  }
+  llm_int8_weights w{emb.data(), g1.data(), be1.data(), g2.data(), be2.data(), qqkv.data(),
+                     sqkv.data(), qo.data(), so.data(), q1.data(), s1.data(), m.b1.data(),
+                     q2.data(), s2.data(), m.b2.data()};
+  return llm_decoder_set_int8_weights(d, &w);
+}
+
+// INT8 directory written by llm_quantize_weights: embedding.f16 [V][hid] fp16;
+// layer_i/{ln1.bin, ln2.bin (fp32 gamma+beta), attn_wqkv.i8 [hid][3hid],
+// attn_wqkv.scale [3hid], attn_wo.i8/.scale, mlp_fc1.i8/.scale, mlp_fc2.i8/.scale,
+// mlp_biases.bin [inter+hid] fp32}.
+extern "C" int llm_quantize_weights(const char* fp32_dir, const char* int8_dir, int num_layers,
+                                    int hidden_dim, int inter_dim, int vocab_size) {
+  LLM_REQUIRE(fp32_dir && int8_dir && num_layers > 0 && hidden_dim > 0 && vocab_size > 0,
+              "llm_quantize_weights: bad arguments");
+  const int L = num_layers, hid = hidden_dim, inter = inter_dim > 0 ? inter_dim : 4 * hidden_dim;
+  Fp32Model m;
+  RET_IF(load_fp32_dir(fp32_dir, L, hid, inter, vocab_size, m));
+  const std::string out = int8_dir;
+  std::vector<uint16_t> emb(m.emb.size());
+  for (size_t i = 0; i < emb.size(); ++i) emb[i] = f32_to_f16_bits(m.emb[i]);
+  if (std::system(("mkdir -p '" + out + "'").c_str()) != 0)
+    return fail(LLM_ERR_IO, "cannot create " + out);
+  RET_IF(write_file(out + "/embedding.f16", emb.data(), emb.size() * 2));
+  for (int l = 0; l < L; ++l) {
+    const std::string p = out + "/layer_" + std::to_string(l);
+    if (std::system(("mkdir -p '" + p + "'").c_str()) != 0)
+      return fail(LLM_ERR_IO, "cannot create " + p);
+    RET_IF(write_file(p + "/ln1.bin", m.ln1.data() + (size_t)l * 2 * hid, (size_t)2 * hid * 4));
+    RET_IF(write_file(p + "/ln2.bin", m.ln2.data() + (size_t)l * 2 * hid, (size_t)2 * hid * 4));
+    struct { const char* name; const float* w; int K, N; } mats[4] = {
+        {"attn_wqkv", m.wqkv.data() + (size_t)l * hid * 3 * hid, hid, 3 * hid},
+        {"attn_wo", m.wo.data() + (size_t)l * hid * hid, hid, hid},
+        {"mlp_fc1", m.w1.data() + (size_t)l * hid * inter, hid, inter},
+        {"mlp_fc2", m.w2.data() + (size_t)l * inter * hid, inter, hid}};
+    for (auto& mt : mats) {
+      std::vector<int8_t> q((size_t)mt.K * mt.N);
+      std::vector<float> s(mt.N);
+      quantize_cols(mt.w, mt.K, mt.N, q.data(), s.data());
+      RET_IF(write_file(p + "/" + mt.name + ".i8", q.data(), q.size()));
+      RET_IF(write_file(p + "/" + mt.name + ".scale", s.data(), s.size() * 4));
+    }
+    std::vector<float> bias(inter + hid);
+    std::memcpy(bias.data(), m.b1.data() + (size_t)l * inter, (size_t)inter * 4);
+    std::memcpy(bias.data() + inter, m.b2.data() + (size_t)l * hid, (size_t)hid * 4);
+    RET_IF(write_file(p + "/mlp_biases.bin", bias.data(), bias.size() * 4));
+  }
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_load_quantized_weights(llm_decoder* d, const char* dir) {
+  LLM_REQUIRE(d && dir, "llm_decoder_load_quantized_weights: NULL");
+  LLM_REQUIRE(d->wdtype == LLM_I8, "llm_decoder_load_quantized_weights: decoder is not INT8");
+  const int L = d->L, hid = d->hid, inter = d->inter, V = d->V;
+  const std::string root = dir;
+  std::vector<char> buf;
+  std::vector<uint16_t> emb((size_t)V * hid);
+  RET_IF(read_file(root + "/embedding.f16", buf, emb.size() * 2));
+  std::memcpy(emb.data(), buf.data(), emb.size() * 2);
+  std::vector<float> g1((size_t)L * hid), be1((size_t)L * hid), g2((size_t)L * hid), be2((size_t)L * hid);
+  std::vector<int8_t> qqkv((size_t)L * hid * 3 * hid), qo((size_t)L * hid * hid),
+      q1((size_t)L * hid * inter), q2((size_t)L * inter * hid);
+  std::vector<float> sqkv((size_t)L * 3 * hid), so((size_t)L * hid), s1((size_t)L * inter),
+      s2((size_t)L * hid), b1((size_t)L * inter), b2((size_t)L * hid);
+  for (int l = 0; l < L; ++l) {
+    const std::string p = root + "/layer_" + std::to_string(l);
+    RET_IF(read_file(p + "/ln1.bin", buf, (size_t)2 * hid * 4));
+    std::memcpy(g1.data() + (size_t)l * hid, buf.data(), hid * 4);
+    std::memcpy(be1.data() + (size_t)l * hid, buf.data() + hid * 4, hid * 4);
+    RET_IF(read_file(p + "/ln2.bin", buf, (size_t)2 * hid * 4));
+    std::memcpy(g2.data() + (size_t)l * hid, buf.data(), hid * 4);
+    std::memcpy(be2.data() + (size_t)l * hid, buf.data() + hid * 4, hid * 4);
+    struct { const char* name; int8_t* q; float* s; int K, N; } mats[4] = {
+        {"attn_wqkv", qqkv.data() + (size_t)l * hid * 3 * hid, sqkv.data() + (size_t)l * 3 * hid, hid, 3 * hid},
+        {"attn_wo", qo.data() + (size_t)l * hid * hid, so.data() + (size_t)l * hid, hid, hid},
+        {"mlp_fc1", q1.data() + (size_t)l * hid * inter, s1.data() + (size_t)l * inter, hid, inter},
+        {"mlp_fc2", q2.data() + (size_t)l * inter * hid, s2.data() + (size_t)l * hid, inter, hid}};
+    for (auto& mt : mats) {
+      RET_IF(read_file(p + "/" + mt.name + ".i8", buf, (size_t)mt.K * mt.N));
+      std::memcpy(mt.q, buf.data(), (size_t)mt.K * mt.N);
+      RET_IF(read_file(p + "/" + mt.name + ".scale", buf, (size_t)mt.N * 4));
+      std::memcpy(mt.s, buf.data(), (size_t)mt.N * 4);
+    }
+    RET_IF(read_file(p + "/mlp_biases.bin", buf, (size_t)(inter + hid) * 4));
+    std::memcpy(b1.data() + (size_t)l * inter, buf.data(), (size_t)inter * 4);
+    std::memcpy(b2.data() + (size_t)l * hid, buf.data() + (size_t)inter * 4, (size_t)hid * 4);
+  }
+  llm_int8_weights w{emb.data(), g1.data(), be1.data(), g2.data(), be2.data(), qqkv.data(),
+                     sqkv.data(), qo.data(), so.data(), q1.data(), s1.data(), b1.data(),
+                     q2.data(), s2.data(), b2.data()};
+  return llm_decoder_set_int8_weights(d, &w);
+}

@@ -64,6 +64,7 @@ int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, l
   entries = (size_t)L * beams * H * max_tiles;
   LLM_HIP_RET(hipMalloc(&d_table, entries * sizeof(int32_t)));
   LLM_HIP_RET(hipMemset(d_table, 0xFF, entries * sizeof(int32_t)));  // -1 (page_table.cpp:22-25)
+  LLM_HIP_RET(hipDeviceSynchronize());  // null-stream memset vs. non-blocking user streams
   h_table.assign(entries, -1);
   dirty_flag.assign(entries, 0);
   refcount.assign((size_t)num_pages, 0);
@@ -360,6 +361,7 @@ extern "C" int kv_cache_clear(kv_cache* c) {
   k.free_list.resize((size_t)k.num_pages);
   for (long long i = 0; i < k.num_pages; ++i) k.free_list[i] = (int32_t)(k.num_pages - 1 - i);
   LLM_HIP_RET(hipMemset(k.d_table, 0xFF, k.entries * sizeof(int32_t)));
+  LLM_HIP_RET(hipDeviceSynchronize());  // null-stream memset vs. non-blocking user streams
   return LLM_OK;
 }
 

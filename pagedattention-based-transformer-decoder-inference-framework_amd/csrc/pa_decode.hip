@@ -32,6 +32,7 @@
 //   * scores are kept in log2 units (q pre-scaled by sm_scale*log2(e)) so
 //     every exponential is one v_exp_f32.
 #include "common.hpp"
+#include "pa_decode.hpp"
 
 #include <algorithm>
 
@@ -42,6 +43,7 @@ struct PaSplitArgs {
   const uint8_t* v_pool;
   const int32_t* page_table;
   const float* q;
+  int q_stride;     // elements between consecutive rows b of q
   float* out;       // DIRECT: final output [B][H][D]
   float* part_acc;  // [B*H*nsplit][D]
   float* part_ml;   // [B*H*nsplit][2]
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
   // q chunk of this lane (dims c*8 .. c*8+7), pre-scaled into log2 units.
   float qv[8];
   {
-    const float* qp = a.q + (size_t)bh * D + c * 8;
+    const float* qp = a.q + (size_t)b * a.q_stride + (size_t)h * D + c * 8;
     const f32x4 q0 = *reinterpret_cast<const f32x4*>(qp);
     const f32x4 q1 = *reinterpret_cast<const f32x4*>(qp + 4);
 #pragma unroll
@@ -171,7 +173,10 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
       for (int i = 0; i < NI; ++i) {
         const float p = valid[i] ? __builtin_amdgcn_exp2f(sc[i] - mnew) : 0.f;
         l += p;
-        const f16x8 vh = __builtin_bit_cast(f16x8, vv[u * NI + i]);
+        // Rows past the context (or of a missing page) may hold stale bits, even
+        // NaN/Inf in a never-written page: select them away (0 * NaN = NaN).
+        const u32x4 vraw = valid[i] ? vv[u * NI + i] : u32x4{0u, 0u, 0u, 0u};
+        const f16x8 vh = __builtin_bit_cast(f16x8, vraw);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, (float)vh[e], acc[e]);
       }
@@ -322,10 +327,10 @@ extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
   return (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
 }
 
-extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
-                         const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
-                         int D, int T, float sm_scale, int pages_per_split, void* workspace,
-                         size_t workspace_bytes, void* stream) {
+int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
+                            const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
+                            int D, int T, float sm_scale, int pages_per_split, void* workspace,
+                            size_t workspace_bytes, hipStream_t st) {
   LLM_REQUIRE(kv != nullptr, "pa_decode: kv view is NULL");
   LLM_REQUIRE(B >= 0 && H > 0 && D > 0 && T >= 0, "pa_decode: bad B/H/D/T");
   if (B == 0) return LLM_OK;
@@ -353,6 +358,7 @@ extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
   a.v_pool = static_cast<const uint8_t*>(kv->v_pool);
   a.page_table = kv->page_table;
   a.q = q;
+  a.q_stride = q_stride;
   a.out = out;
   a.beam_ids = beam_ids;
   a.context_lens = context_lens;
@@ -372,7 +378,6 @@ extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
     a.part_acc = static_cast<float*>(workspace);
     a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   }
-  hipStream_t st = as_stream(stream);
   hipError_t e;
   switch (D) {
     case 32: e = dispatch_ts<32>(a, TS, direct, st); break;
@@ -387,4 +392,12 @@ extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
     LLM_HIP_RET(hipGetLastError());
   }
   return LLM_OK;
+}
+
+extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
+                         const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
+                         int D, int T, float sm_scale, int pages_per_split, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  return pa_decode_internal(kv, q, H * D, out, beam_ids, context_lens, B, H, D, T, sm_scale,
+                            pages_per_split, workspace, workspace_bytes, as_stream(stream));
 }

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kRowThreads) void quantize_rows_kernel(const float*
 __global__ __launch_bounds__(kRowThreads) void layernorm_quant_kernel(
     const float* __restrict__ x, int cols, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
-    float* __restrict__ inv_scale) {
+    float* __restrict__ inv_scale, _Float16* __restrict__ out16) {
   extern __shared__ __attribute__((aligned(16))) float row[];  // cols floats
   __shared__ float sh[kRowThreads / 64];
   const int r = blockIdx.x;
@@ -88,6 +88,7 @@ __global__ __launch_bounds__(kRowThreads) void layernorm_quant_kernel(
     row[i] = y;
     am = fmaxf(am, fabsf(y));
     if (out) out[(size_t)r * cols + i] = y;
+    if (out16) out16[(size_t)r * cols + i] = (_Float16)y;
   }
   if (q) {
     am = block_reduce_max(am, sh);
@@ -169,6 +170,20 @@ __global__ __launch_bounds__(kRowThreads) void kv_append_kernel(
   }
 }
 
+__global__ void to_f16_kernel(const float* __restrict__ x, size_t n, _Float16* __restrict__ y) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    y[i] = (_Float16)x[i];
+}
+
+// After a step: every row's next position / context length moves by one.
+__global__ void advance_kernel(int32_t* __restrict__ pos, int32_t* __restrict__ ctx, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    pos[i] += 1;
+    ctx[i] += 1;
+  }
+}
+
 // page_table[idx[i]] = val[i] (device half of PageTable sync).
 __global__ void scatter_i32_kernel(int32_t* __restrict__ dst, const int64_t* __restrict__ idx,
                                    const int32_t* __restrict__ val, int n) {
@@ -207,7 +222,29 @@ hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const floa
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
                                   hipStream_t st) {
   hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
-                     (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv);
+                     (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv,
+                     (_Float16*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
+                                const float* b, float eps, void* out16, hipStream_t st) {
+  hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
+                     (size_t)cols * sizeof(float), st, x, cols, g, b, eps, (float*)nullptr,
+                     (int8_t*)nullptr, (float*)nullptr, static_cast<_Float16*>(out16));
+  return hipGetLastError();
+}
+
+hipError_t launch_to_f16(const float* x, size_t n, void* y, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(to_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n,
+                     static_cast<_Float16*>(y));
+  return hipGetLastError();
+}
+
+hipError_t launch_advance(int32_t* pos, int32_t* ctx, int n, hipStream_t st) {
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, pos, ctx, n);
   return hipGetLastError();
 }
 

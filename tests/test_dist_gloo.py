@@ -1,0 +1,117 @@
+"""N > 1 path on CPU: world_size-2 gloo processes shard the rows, step the
+(oracle) decoder on their shard and gather logits / generated ids to rank 0;
+rank 0's result must equal a single-process run over all rows bit-exactly."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model():
+    from oracle.oracle import Oracle, synthetic_int8_model
+    o = Oracle()
+    return o, synthetic_int8_model(o, L=2, H=2, D=64, V=300, max_seq=32, seed=21)
+
+
+class _OracleGen:
+    """generate_batch over the oracle decoder (greedy, lockstep rows)."""
+
+    def __init__(self, o, w, n):
+        from oracle.oracle import OracleDecoder
+        self.dec = OracleDecoder(o, w, n) if n else None
+        self.n = n
+
+    def generate_batch(self, prompts, max_gen_len, temperature=1.0):
+        steps = max(len(p) for p in prompts) + max_gen_len - 1
+        res = [list(p) for p in prompts]
+        nxt = [0] * self.n
+        for s in range(steps):
+            tok = [p[s] if s < len(p) else nxt[b] for b, p in enumerate(prompts)]
+            _, _, n = self.dec.step(np.array(tok, np.int32), np.full(self.n, s, np.int32))
+            nxt = [int(x) for x in n]
+            for b in range(self.n):
+                if len(prompts[b]) - 1 <= s and len(res[b]) < len(prompts[b]) + max_gen_len:
+                    res[b].append(nxt[b])
+        return res
+
+
+def _worker(rank, world, port, rows, steps, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (str(ROOT), str(PKG)):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    from dist_decode import LogitsGatherer, distributed_generate, shard_range
+    from oracle.oracle import OracleDecoder
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o, w = _model()
+    lo, hi = shard_range(rows, world, rank)
+    dec = OracleDecoder(o, w, hi - lo)
+    sizes = [shard_range(rows, world, r)[1] - shard_range(rows, world, r)[0] for r in range(world)]
+    g = LogitsGatherer((hi - lo, w["cfg"]["V"]), torch.float32, "cpu", world, rank, sizes,
+                       keep=True)
+    rng = np.random.default_rng(0)
+    all_toks = rng.integers(0, w["cfg"]["V"], (steps, rows)).astype(np.int32)
+    for s in range(steps):
+        buf = g.buffer()
+        _, logits, _ = dec.step(all_toks[s, lo:hi], np.full(hi - lo, s, np.int32))
+        buf.copy_(torch.from_numpy(logits))
+        g.push()
+    collected = [t.numpy() for t in g.finish()]
+    prompts = [[int(x) for x in rng.integers(0, 300, n)] for n in (3, 1, 4, 2, 5)]
+    gen = distributed_generate(lambda n: _OracleGen(o, w, n), prompts, 4)
+    if rank == 0:
+        q.put((collected, gen, all_toks, prompts))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shard_and_gather():
+    import torch.multiprocessing as mp
+    rows, steps, world = 5, 4, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rows, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    collected, gen, all_toks, prompts = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference over all rows
+    from oracle.oracle import OracleDecoder
+    o, w = _model()
+    ref = OracleDecoder(o, w, rows)
+    assert len(collected) == steps
+    for s in range(steps):
+        _, logits, _ = ref.step(all_toks[s], np.full(rows, s, np.int32))
+        np.testing.assert_array_equal(collected[s], logits)
+    ref_gen = _OracleGen(o, w, len(prompts)).generate_batch(prompts, 4)
+    assert gen == ref_gen
+
+
+def test_shard_range_covers_batch():
+    sys.path.insert(0, str(PKG))
+    from dist_decode import shard_range
+    for n in (0, 1, 5, 64, 512, 513):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,139 @@
+"""KV page cache / page table (kv_cache/page_table.hpp:5-37,
+kv_cache/kv_tile_cache.hpp:9-41 semantics) through the C ABI and the pybind11
+classes: index arithmetic bit-exact against the oracle, free-list allocation,
+beam fork with copy-on-write, save/load, and attention over a forked cache."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from _util import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def test_page_table_semantics(gpu, oracle):
+    import torch
+    import llm_decoder
+    pt = llm_decoder.PageTable()
+    pt.init(2, 3, 5)
+    assert pt.lookup(0, 0, 0) == -1  # init to -1 (page_table.cpp:22-25)
+    pt.assign(1, 2, 4, 7)
+    pt.assign(0, 1, 3, 2)
+    assert pt.lookup(1, 2, 4) == 7 and pt.lookup(0, 1, 3) == 2
+    assert pt.lookup(2, 0, 0) == -1 and pt.lookup(0, 3, 0) == -1  # out of range -> -1
+    pt.remove(1, 2, 4)
+    pt.sync_to_gpu()
+    torch.cuda.synchronize()
+    # device copy equals the host mirror (single source of truth); index
+    # = beam*(H*NT) + head*NT + tile (page_table.hpp:41)
+    host = np.full(30, -1, np.int32)
+    host[0 * 15 + 1 * 5 + 3] = 2
+    hip_ptr = pt.device_data()
+    arr = (ctypes.c_int32 * 30)()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(ctypes.addressof(arr), ctypes.c_void_p(hip_ptr), 120, 2) == 0
+    np.testing.assert_array_equal(np.frombuffer(arr, np.int32), host)
+    pt.clear()
+    assert pt.lookup(0, 1, 3) == -1
+
+
+def test_kv_cache_alloc_fork_cow(gpu):
+    import llm_capi
+    lib = llm_capi.load()
+    h = ctypes.c_void_p()
+    llm_capi.check(lib.kv_cache_create(2, 3, 2, 64, 16, 8, 40, ctypes.byref(h)))
+    try:
+        assert lib.kv_cache_free_pages(h) == 40
+        llm_capi.check(lib.kv_cache_reserve(h, 0, 33))  # 3 tiles x 2 heads x 2 layers
+        assert lib.kv_cache_free_pages(h) == 40 - 12
+        pages = {lib.kv_cache_lookup(h, l, 0, hh, t) for l in range(2) for hh in range(2) for t in range(3)}
+        assert len(pages) == 12 and -1 not in pages  # distinct ids (no map.size() aliasing)
+        llm_capi.check(lib.kv_cache_fork(h, 0, 1))
+        assert lib.kv_cache_free_pages(h) == 40 - 12  # shared, not copied
+        assert lib.kv_cache_lookup(h, 1, 1, 1, 2) == lib.kv_cache_lookup(h, 1, 0, 1, 2)
+        # writing into beam 1's shared last tile copies it first (copy-on-write)
+        k = np.ones((1, 2, 64), np.float16).view(np.uint16)
+        llm_capi.check(lib.kv_cache_write_tokens(h, 0, 1, 33, 1, k.ctypes.data, k.ctypes.data))
+        assert lib.kv_cache_lookup(h, 0, 1, 0, 2) != lib.kv_cache_lookup(h, 0, 0, 0, 2)
+        assert lib.kv_cache_lookup(h, 1, 1, 0, 2) == lib.kv_cache_lookup(h, 1, 0, 0, 2)  # other layer still shared
+        assert lib.kv_cache_free_pages(h) == 40 - 12 - 2
+        llm_capi.check(lib.kv_cache_release(h, 0))
+        assert lib.kv_cache_free_pages(h) == 40 - 12 - 2 + 2  # only pages no other beam holds
+        llm_capi.check(lib.kv_cache_release(h, 1))
+        assert lib.kv_cache_free_pages(h) == 40
+        # exhaustion is an error, not a silent eviction
+        llm_capi.check(lib.kv_cache_reserve(h, 2, 16 * 8))  # 32 of 40 pages
+        assert lib.kv_cache_reserve(h, 0, 16 * 8) == llm_capi.LLM_ERR_OOM
+    finally:
+        lib.kv_cache_destroy(h)
+
+
+def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
+    """Beams forked from a shared prefix, then diverging tokens written with
+    COW; pa_decode over the cache (beam_ids routing) matches the oracle on the
+    pools read back; save/load round-trips the cache bit-exactly."""
+    import torch
+    import llm_capi
+    import llm_decoder
+    rng = np.random.default_rng(3)
+    H, D, TS, prefix, tail, beams = 2, 128, 16, 40, 9, 3
+    kv = llm_decoder.KVTileCache()
+    kv.init(num_pages=64, tile_size=TS, head_dim=D, num_layers=1, num_beams=beams,
+            num_heads=H, max_tiles=8)
+    kp = rng.standard_normal((prefix, H, D)).astype(np.float16)
+    vp = rng.standard_normal((prefix, H, D)).astype(np.float16)
+    kv.write_tokens(0, 0, 0, kp.view(np.uint16), vp.view(np.uint16))
+    for b in (1, 2):
+        kv.fork(0, b)
+    tails = {}
+    for b in range(beams):
+        kt = rng.standard_normal((tail, H, D)).astype(np.float16)
+        vt = rng.standard_normal((tail, H, D)).astype(np.float16)
+        kv.write_tokens(0, b, prefix, kt.view(np.uint16), vt.view(np.uint16))
+        tails[b] = (kt, vt)
+    T = prefix + tail
+    view = kv.view(0)
+    num_pages = view["num_pages"]
+    lib = llm_capi.load()
+    # read back pools and table through torch
+    def dev_copy(ptr, n, dtype):
+        t = torch.empty(n, dtype=dtype, device="cuda")
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr),
+                             n * t.element_size(), 3) == 0
+        return t
+    kpool = dev_copy(view["k_pool"], num_pages * TS * D, torch.float16).reshape(num_pages, TS, D)
+    vpool = dev_copy(view["v_pool"], num_pages * TS * D, torch.float16).reshape(num_pages, TS, D)
+    table = dev_copy(view["page_table"], beams * H * 8, torch.int32).reshape(beams, H, 8)
+    # the pools hold exactly what was written, per beam
+    for b in range(beams):
+        for t in range(T):
+            page = kv.lookup(b, 1, t // TS)
+            want = kp[t, 1] if t < prefix else tails[b][0][t - prefix, 1]
+            np.testing.assert_array_equal(kpool[page, t % TS].cpu().numpy(), want)
+    q = (rng.standard_normal((4, H, D)) * D ** -0.25).astype(np.float32)
+    beam_ids = np.array([2, 0, 1, 2], np.int32)
+    out = llm_capi.pa_decode(torch.from_numpy(q).cuda(), kpool, vpool, table, T=T,
+                             beam_ids=torch.from_numpy(beam_ids).cuda()).cpu().numpy()
+    ref = oracle.paged_attention(q, kpool.float().cpu().numpy(), vpool.float().cpu().numpy(),
+                                 table.cpu().numpy(), T=T, beam_ids=beam_ids)
+    assert rel_err(out, ref) < 1e-3
+    # save / load round trip
+    path = str(tmp_path / "kv.bin")
+    kv.save_to_file(path)
+    kv2 = llm_decoder.KVTileCache()
+    kv2.init(num_pages=64, tile_size=TS, head_dim=D, num_layers=1, num_beams=beams,
+             num_heads=H, max_tiles=8)
+    kv2.load_from_file(path)
+    for b in range(beams):
+        for t in range(4):
+            assert kv2.lookup(b, 0, t) == kv.lookup(b, 0, t)
+    v2 = kv2.view(0)
+    kpool2 = dev_copy(v2["k_pool"], num_pages * TS * D, torch.float16).reshape(num_pages, TS, D)
+    used = sorted({kv.lookup(b, h, t) for b in range(beams) for h in range(H) for t in range(4)})
+    # bitwise (rows past the written tokens are never-written bits, possibly NaN)
+    assert torch.equal(kpool2[used].view(torch.int16), kpool[used].view(torch.int16))
+    assert kv2.free_pages() == kv.free_pages()

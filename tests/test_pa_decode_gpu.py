@@ -170,3 +170,24 @@ def test_pa_decode_rejects_bad_shapes(gpu):
     rc = lib.pa_decode(ctypes.byref(view), llm_capi.ptr(q), llm_capi.ptr(out), None, None,
                        1, 2, 48, 16, 1.0, 0, None, 0, llm_capi.stream_ptr())
     assert rc == llm_capi.LLM_ERR_INVALID
+
+
+def test_pa_decode_stale_nan_rows_ignored(gpu, oracle):
+    """Rows of a page past the context hold whatever was there before (a fresh
+    hipMalloc can hold NaN/Inf bit patterns); they must not leak into out."""
+    import llm_capi
+    rng = np.random.default_rng(17)
+    B, H, D, T, ts = 3, 2, 128, 200, 16  # 200 = 12 full pages + 8 rows
+    q, kp, vp, pt = _random_case(rng, B, H, D, T, ts)
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T)
+    last = pt[:, :, T // ts]
+    kp[last, T % ts:] = np.nan
+    vp[last, T % ts:] = np.inf
+    unused = np.setdiff1d(np.arange(kp.shape[0]), pt.ravel())
+    kp[unused] = np.nan
+    vp[unused] = np.nan
+    for pps in (0, 4):
+        out = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T,
+                                 pages_per_split=pps).cpu().numpy()
+        assert np.isfinite(out).all()
+        assert rel_err(out, ref) < RTOL
