@@ -18,6 +18,7 @@
 // page every page_size tokens, copy-on-write of forked pages) happens on the
 // host between replays and is pushed with kv_cache_sync().
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -56,6 +57,11 @@ struct DevBuf {
 
 #define RET_IF(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
 }  // namespace
 
 struct llm_decoder {
@@ -93,11 +99,28 @@ struct llm_decoder {
   ~llm_decoder() {
     if (graph) (void)hipGraphExecDestroy(graph);
     if (kv) kv_cache_destroy(kv);
+    for (hipEvent_t e : ev_attn) (void)hipEventDestroy(e);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (stream2) (void)hipStreamDestroy(stream2);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  int layer_forward_int8(int l, hipStream_t st);
-  int layer_forward_f16(int l, hipStream_t st);
+  // micro-batch overlap (see enqueue_step)
+  int microbatches = 1;
+  bool pingpong = true;
+  bool use_graph = true;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::vector<hipEvent_t> ev_attn;  // [L][2]
+  DevBuf<uint8_t> attn_ws2;
+  int qa_ld = 0;
+
+  int layer_pre(int l, hipStream_t st, const struct MicroBatch& mb);
+  int layer_attn(int l, hipStream_t st, const struct MicroBatch& mb);
+  int layer_post(int l, hipStream_t st, const struct MicroBatch& mb);
+  int step_head(hipStream_t st, const struct MicroBatch& mb);
+  int step_tail(hipStream_t st, const struct MicroBatch& mb);
   int enqueue_step(hipStream_t st);
   int run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host, hipStream_t st);
 };
@@ -146,9 +169,28 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->tokens.alloc((size_t)B));
   RET_IF(d->pos.alloc((size_t)B));
   RET_IF(d->ctx.alloc((size_t)B));
-  d->pps = pa_pages_per_split(B, d->H, c.max_seq_len, d->TS, d->max_tiles);
-  d->attn_ws_bytes = pa_decode_workspace_bytes(B, d->H, d->D, d->max_tiles, d->pps);
+  d->pps = 0;  // balanced splits derived on device from each row's context
+  d->attn_ws_bytes = 16;
+  for (int b = 1; b <= B; ++b)  // any batch / micro-batch size up to max_batch
+    d->attn_ws_bytes = std::max(d->attn_ws_bytes,
+                                pa_decode_workspace_bytes(b, d->H, d->D, d->max_tiles, 0));
   RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
+  d->qa_ld = std::max(hid, inter);
+  // micro-batch overlap: LLM_MICROBATCHES=1|2 (default 2 for batches >= 2),
+  // LLM_MB_PINGPONG=0|1, LLM_GRAPH=0|1 (eager launches, for profiling)
+  d->microbatches = env_int("LLM_MICROBATCHES", 2);
+  d->pingpong = env_int("LLM_MB_PINGPONG", 1) != 0;
+  d->use_graph = env_int("LLM_GRAPH", 1) != 0;
+  if (d->microbatches >= 2 && B >= 2) {
+    LLM_HIP_RET(hipStreamCreateWithFlags(&d->stream2, hipStreamNonBlocking));
+    LLM_HIP_RET(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+    LLM_HIP_RET(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+    d->ev_attn.resize((size_t)2 * d->L);
+    for (auto& e : d->ev_attn) LLM_HIP_RET(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    RET_IF(d->attn_ws2.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
+  } else {
+    d->microbatches = 1;
+  }
   d->h_pos.assign(B, 0);
   *out = d.release();
   return LLM_OK;
@@ -248,65 +290,142 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
 // ---------------------------------------------------------------------------
 // step
 // ---------------------------------------------------------------------------
-int llm_decoder::layer_forward_int8(int l, hipStream_t st) {
-  const int B = batch;
+// Rows [r0, r0 + n) of the batch: every activation / state buffer is
+// row-indexed, so a micro-batch is a set of offset pointers (plus its own
+// attention workspace).
+struct MicroBatch {
+  int r0 = 0, n = 0;
+  uint8_t* attn_ws = nullptr;
+};
+
+int llm_decoder::layer_pre(int l, hipStream_t st, const MicroBatch& mb) {
+  const int r0 = mb.r0, B = mb.n;
   const size_t lh = (size_t)l * hid;
-  const int qa_ld = std::max(hid, inter);
-  (void)qa_ld;
-  // LN1 + quant (rows of `hid` int8 at stride hid)
-  LLM_HIP_RET(launch_layernorm_quant(x.p, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
-                                     qa.p, sa.p, st));
-  RET_IF(i8_gemm(qa.p, hid, wqkv.p + sz_qkv * l, nullptr, qkv.p, B, 3 * hid, hid, sa.p,
-                 sw_qkv.p + (size_t)l * 3 * hid, nullptr, LLM_ACT_NONE, st));
+  float* xr = x.p + (size_t)r0 * hid;
+  float* qkvr = qkv.p + (size_t)r0 * 3 * hid;
+  if (wdtype == LLM_I8) {
+    int8_t* qar = qa.p + (size_t)r0 * qa_ld;
+    float* sar = sa.p + r0;
+    LLM_HIP_RET(launch_layernorm_quant(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
+                                       qar, sar, st));
+    RET_IF(i8_gemm(qar, hid, wqkv.p + sz_qkv * l, nullptr, qkvr, B, 3 * hid, hid, sar,
+                   sw_qkv.p + (size_t)l * 3 * hid, nullptr, LLM_ACT_NONE, st));
+  } else {
+    uint16_t* a16r = a16.p + (size_t)r0 * qa_ld;
+    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, a16r, st));
+    RET_IF(f16_gemm(a16r, hid, wqkv.p + sz_qkv * l, qkvr, B, 3 * hid, hid, nullptr, LLM_ACT_NONE,
+                    st));
+  }
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
-  LLM_HIP_RET(launch_kv_append(qkv.p, B, H, D, pos.p, view.page_table, view.num_beams,
-                               view.max_tiles, TS, view.num_pages, kv_cache_k_pool(kv),
-                               kv_cache_v_pool(kv), st));
-  RET_IF(pa_decode_internal(&view, qkv.p, 3 * hid, o.p, nullptr, ctx.p, B, H, D,
-                            cfg.max_seq_len, cfg.attn_scale, pps, attn_ws.p, attn_ws_bytes, st));
-  LLM_HIP_RET(launch_quantize_rows(o.p, B, hid, qa.p, sa.p, st));
-  RET_IF(i8_gemm(qa.p, hid, wo.p + sz_o * l, nullptr, x.p, B, hid, hid, sa.p, sw_o.p + lh,
-                 nullptr, LLM_ACT_NONE, st));
-  LLM_HIP_RET(launch_layernorm_quant(x.p, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
-                                     qa.p, sa.p, st));
-  RET_IF(i8_gemm(qa.p, hid, w1.p + sz_1 * l, nullptr, h1.p, B, inter, hid, sa.p,
-                 sw1.p + (size_t)l * inter, b1.p + (size_t)l * inter, LLM_ACT_RELU, st));
-  LLM_HIP_RET(launch_quantize_rows(h1.p, B, inter, qa.p, sa.p, st));
-  RET_IF(i8_gemm(qa.p, inter, w2.p + sz_2 * l, nullptr, x.p, B, hid, inter, sa.p, sw2.p + lh,
-                 b2.p + lh, LLM_ACT_NONE, st));
+  LLM_HIP_RET(launch_kv_append(qkvr, B, H, D, pos.p + r0,
+                               view.page_table + (size_t)r0 * H * view.max_tiles,
+                               view.num_beams - r0, view.max_tiles, TS, view.num_pages,
+                               kv_cache_k_pool(kv), kv_cache_v_pool(kv), st));
   return LLM_OK;
 }
 
-int llm_decoder::layer_forward_f16(int l, hipStream_t st) {
-  const int B = batch;
-  const size_t lh = (size_t)l * hid;
-  LLM_HIP_RET(launch_layernorm_f16(x.p, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, a16.p, st));
-  RET_IF(f16_gemm(a16.p, hid, wqkv.p + sz_qkv * l, qkv.p, B, 3 * hid, hid, nullptr, LLM_ACT_NONE,
-                  st));
+int llm_decoder::layer_attn(int l, hipStream_t st, const MicroBatch& mb) {
+  const int r0 = mb.r0, B = mb.n;
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
-  LLM_HIP_RET(launch_kv_append(qkv.p, B, H, D, pos.p, view.page_table, view.num_beams,
-                               view.max_tiles, TS, view.num_pages, kv_cache_k_pool(kv),
-                               kv_cache_v_pool(kv), st));
-  RET_IF(pa_decode_internal(&view, qkv.p, 3 * hid, o.p, nullptr, ctx.p, B, H, D,
-                            cfg.max_seq_len, cfg.attn_scale, pps, attn_ws.p, attn_ws_bytes, st));
-  LLM_HIP_RET(launch_to_f16(o.p, (size_t)B * hid, a16.p, st));
-  RET_IF(f16_gemm(a16.p, hid, wo.p + sz_o * l, x.p, B, hid, hid, nullptr, LLM_ACT_NONE, st));
-  LLM_HIP_RET(launch_layernorm_f16(x.p, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, a16.p, st));
-  RET_IF(f16_gemm(a16.p, hid, w1.p + sz_1 * l, h1.p, B, inter, hid, b1.p + (size_t)l * inter,
-                  LLM_ACT_RELU, st));
-  LLM_HIP_RET(launch_to_f16(h1.p, (size_t)B * inter, a16.p, st));
-  RET_IF(f16_gemm(a16.p, inter, w2.p + sz_2 * l, x.p, B, hid, inter, b2.p + lh, LLM_ACT_NONE, st));
+  view.page_table += (size_t)r0 * H * view.max_tiles;  // rows of this micro-batch
+  view.num_beams -= r0;
+  return pa_decode_internal(&view, qkv.p + (size_t)r0 * 3 * hid, 3 * hid, o.p + (size_t)r0 * hid,
+                            nullptr, ctx.p + r0, B, H, D, cfg.max_seq_len, cfg.attn_scale, pps,
+                            mb.attn_ws, attn_ws_bytes, st);
+}
+
+int llm_decoder::layer_post(int l, hipStream_t st, const MicroBatch& mb) {
+  const int r0 = mb.r0, B = mb.n;
+  const size_t lh = (size_t)l * hid;
+  float* xr = x.p + (size_t)r0 * hid;
+  float* orow = o.p + (size_t)r0 * hid;
+  float* h1r = h1.p + (size_t)r0 * inter;
+  if (wdtype == LLM_I8) {
+    int8_t* qar = qa.p + (size_t)r0 * qa_ld;
+    float* sar = sa.p + r0;
+    LLM_HIP_RET(launch_quantize_rows(orow, B, hid, qar, sar, st));
+    RET_IF(i8_gemm(qar, hid, wo.p + sz_o * l, nullptr, xr, B, hid, hid, sar, sw_o.p + lh, nullptr,
+                   LLM_ACT_NONE, st));
+    LLM_HIP_RET(launch_layernorm_quant(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
+                                       qar, sar, st));
+    RET_IF(i8_gemm(qar, hid, w1.p + sz_1 * l, nullptr, h1r, B, inter, hid, sar,
+                   sw1.p + (size_t)l * inter, b1.p + (size_t)l * inter, LLM_ACT_RELU, st));
+    LLM_HIP_RET(launch_quantize_rows(h1r, B, inter, qar, sar, st));
+    RET_IF(i8_gemm(qar, inter, w2.p + sz_2 * l, nullptr, xr, B, hid, inter, sar, sw2.p + lh,
+                   b2.p + lh, LLM_ACT_NONE, st));
+  } else {
+    uint16_t* a16r = a16.p + (size_t)r0 * qa_ld;
+    LLM_HIP_RET(launch_to_f16(orow, (size_t)B * hid, a16r, st));
+    RET_IF(f16_gemm(a16r, hid, wo.p + sz_o * l, xr, B, hid, hid, nullptr, LLM_ACT_NONE, st));
+    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, a16r, st));
+    RET_IF(f16_gemm(a16r, hid, w1.p + sz_1 * l, h1r, B, inter, hid, b1.p + (size_t)l * inter,
+                    LLM_ACT_RELU, st));
+    LLM_HIP_RET(launch_to_f16(h1r, (size_t)B * inter, a16r, st));
+    RET_IF(f16_gemm(a16r, inter, w2.p + sz_2 * l, xr, B, hid, inter, b2.p + lh, LLM_ACT_NONE, st));
+  }
   return LLM_OK;
 }
 
+int llm_decoder::step_head(hipStream_t st, const MicroBatch& mb) {
+  return launch_embed(emb.p, tokens.p + mb.r0, mb.n, hid, V, x.p + (size_t)mb.r0 * hid, st) ==
+                 hipSuccess
+             ? LLM_OK
+             : fail(LLM_ERR_HIP, "embed launch");
+}
+
+int llm_decoder::step_tail(hipStream_t st, const MicroBatch& mb) {
+  const int r0 = mb.r0;
+  float* lg = logits.p + (size_t)r0 * V;
+  RET_IF(lm_head(x.p + (size_t)r0 * hid, emb.p, lg, mb.n, V, hid, st));
+  LLM_HIP_RET(launch_argmax(lg, mb.n, V, tokens.p + r0, nullptr, 0, st));  // next tokens in place
+  LLM_HIP_RET(launch_advance(pos.p + r0, ctx.p + r0, mb.n, st));
+  return LLM_OK;
+}
+
+// One decode step.  With two micro-batches the rows are split in halves that
+// run on two streams (captured as two graph branches); their paged-attention
+// launches are ordered ping-pong (A.attn(l) -> B.attn(l) -> A.attn(l+1) ...), so
+// while one half streams its KV pages the other half's latency-bound glue
+// (LayerNorm, quantisation, weight GEMMs, KV append, split merge) runs beside
+// it instead of between attention launches.
 int llm_decoder::enqueue_step(hipStream_t st) {
-  LLM_HIP_RET(launch_embed(emb.p, tokens.p, batch, hid, V, x.p, st));
-  for (int l = 0; l < L; ++l) RET_IF(wdtype == LLM_I8 ? layer_forward_int8(l, st) : layer_forward_f16(l, st));
-  RET_IF(lm_head(x.p, emb.p, logits.p, batch, V, hid, st));
-  LLM_HIP_RET(launch_argmax(logits.p, batch, V, tokens.p, nullptr, 0, st));  // next tokens in place
-  LLM_HIP_RET(launch_advance(pos.p, ctx.p, batch, st));
+  const int nmb = (batch >= 2 && microbatches >= 2) ? 2 : 1;
+  MicroBatch mbs[2];
+  if (nmb == 1) {
+    mbs[0] = {0, batch, attn_ws.p};
+    RET_IF(step_head(st, mbs[0]));
+    for (int l = 0; l < L; ++l) {
+      RET_IF(layer_pre(l, st, mbs[0]));
+      RET_IF(layer_attn(l, st, mbs[0]));
+      RET_IF(layer_post(l, st, mbs[0]));
+    }
+    return step_tail(st, mbs[0]);
+  }
+  const int h0 = (batch + 1) / 2;
+  mbs[0] = {0, h0, attn_ws.p};
+  mbs[1] = {h0, batch - h0, attn_ws2.p};
+  hipStream_t S[2] = {st, stream2};
+  LLM_HIP_RET(hipEventRecord(ev_fork, st));
+  LLM_HIP_RET(hipStreamWaitEvent(stream2, ev_fork, 0));
+  for (int j = 0; j < 2; ++j) RET_IF(step_head(S[j], mbs[j]));
+  for (int l = 0; l < L; ++l) {
+    for (int j = 0; j < 2; ++j) {
+      RET_IF(layer_pre(l, S[j], mbs[j]));
+      if (pingpong) {
+        // A.attn(l) after B.attn(l-1); B.attn(l) after A.attn(l)
+        if (j == 0 && l > 0) LLM_HIP_RET(hipStreamWaitEvent(S[0], ev_attn[2 * (l - 1) + 1], 0));
+        if (j == 1) LLM_HIP_RET(hipStreamWaitEvent(S[1], ev_attn[2 * l], 0));
+      }
+      RET_IF(layer_attn(l, S[j], mbs[j]));
+      if (pingpong) LLM_HIP_RET(hipEventRecord(ev_attn[2 * l + j], S[j]));
+      RET_IF(layer_post(l, S[j], mbs[j]));
+    }
+  }
+  for (int j = 0; j < 2; ++j) RET_IF(step_tail(S[j], mbs[j]));
+  LLM_HIP_RET(hipEventRecord(ev_join, stream2));
+  LLM_HIP_RET(hipStreamWaitEvent(st, ev_join, 0));
   return LLM_OK;
 }
 
@@ -329,21 +448,27 @@ int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t
     LLM_HIP_RET(hipMemcpyAsync(tokens.p, tokens_host, sizeof(int32_t) * batch,
                                hipMemcpyHostToDevice, st));
   }
-  if (graph_batch != batch) {
-    if (graph) { (void)hipGraphExecDestroy(graph); graph = nullptr; }
-    hipGraph_t g;
-    LLM_HIP_RET(hipStreamSynchronize(st));
-    LLM_HIP_RET(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_step(stream);
-    hipError_t e = hipStreamEndCapture(stream, &g);
-    if (rc) return rc;
-    if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
-    e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(e));
-    graph_batch = batch;
+  if (!use_graph) {
+    RET_IF(enqueue_step(st));
+  } else {
+    if (graph_batch != batch) {
+      if (graph) { (void)hipGraphExecDestroy(graph); graph = nullptr; }
+      hipGraph_t g;
+      LLM_HIP_RET(hipStreamSynchronize(st));
+      LLM_HIP_RET(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      int rc = enqueue_step(stream);
+      hipError_t e = hipStreamEndCapture(stream, &g);
+      if (rc) return rc;
+      if (e != hipSuccess)
+        return fail(LLM_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+      e = hipGraphInstantiate(&graph, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (e != hipSuccess)
+        return fail(LLM_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(e));
+      graph_batch = batch;
+    }
+    LLM_HIP_RET(hipGraphLaunch(graph, st));
   }
-  LLM_HIP_RET(hipGraphLaunch(graph, st));
   for (int b = 0; b < batch; ++b) h_pos[b] += 1;
   if (logits_dev)
     LLM_HIP_RET(hipMemcpyAsync(logits_dev, logits.p, sizeof(float) * batch * V,
@@ -383,7 +508,7 @@ extern "C" int llm_decoder_begin_synthetic(llm_decoder* d, int batch, int contex
     std::lock_guard<std::mutex> gk(k->mu);
     if (shuffle) {  // non-contiguous page gather (shuffled page pool, seed 7)
       std::mt19937_64 rng(seed ^ 7);
-      std::shuffle(k->free_list.begin(), k->free_list.end(), rng);
+      for (auto& f : k->free_lists) std::shuffle(f.begin(), f.end(), rng);
     }
   }
   for (int b = 0; b < batch; ++b) RET_IF(kv_cache_reserve(d->kv, b, context_len));

@@ -9,7 +9,7 @@
 //     kv_cache_sync() with a scatter of the dirty entries (the reference's
 //     assign() writes only the device, remove() only the host, and
 //     sync_to_gpu() overwrites the device, page_table.cpp:49-66);
-//   * a free-list page allocator with per-page refcounts (the reference's
+//   * a free-list page allocator (one list per layer zone) with per-page refcounts (the reference's
 //     page id = map.size() aliases live pages after an eviction,
 //     kv_tile_cache.cpp:71), so beams can fork and share prefix pages;
 //   * copy-on-write of a shared page before a token is written into it.
@@ -68,8 +68,7 @@ int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, l
   h_table.assign(entries, -1);
   dirty_flag.assign(entries, 0);
   refcount.assign((size_t)num_pages, 0);
-  free_list.resize((size_t)num_pages);
-  for (long long i = 0; i < num_pages; ++i) free_list[i] = (int32_t)(num_pages - 1 - i);
+  reset_free_lists();
   LLM_HIP_RET(hipEventCreateWithFlags(&staging_done, hipEventDisableTiming));
   return LLM_OK;
 }
@@ -99,21 +98,48 @@ void KvCache::set_entry(size_t idx, int32_t page) {
   }
 }
 
-int KvCache::alloc_page(int32_t* out) {
-  if (free_list.empty())
-    return fail(LLM_ERR_OOM, "kv_cache: page pool exhausted (" + std::to_string(num_pages) +
-                                 " pages)");
-  *out = free_list.back();
-  free_list.pop_back();
-  refcount[*out] = 1;
-  return LLM_OK;
+void KvCache::reset_free_lists() {
+  const int zones = (int)std::max<long long>(1, std::min<long long>(L, num_pages));
+  zone_pages = num_pages / zones;
+  free_lists.assign(zones, {});
+  for (long long p = num_pages - 1; p >= 0; --p)  // pop_back hands out low ids first
+    if (refcount[p] == 0) free_lists[zone_of_page((int32_t)p)].push_back((int32_t)p);
+}
+
+long long KvCache::free_count() const {
+  long long n = 0;
+  for (const auto& f : free_lists) n += (long long)f.size();
+  return n;
+}
+
+bool KvCache::take_free(int32_t page) {
+  auto& f = free_lists[zone_of_page(page)];
+  auto it = std::find(f.begin(), f.end(), page);
+  if (it == f.end()) return false;
+  f.erase(it);
+  return true;
+}
+
+int KvCache::alloc_page(int layer, int32_t* out) {
+  const int z0 = zone_of_layer(std::max(layer, 0));
+  const int nz = (int)free_lists.size();
+  for (int i = 0; i < nz; ++i) {
+    auto& f = free_lists[(z0 + i) % nz];
+    if (f.empty()) continue;
+    *out = f.back();
+    f.pop_back();
+    refcount[*out] = 1;
+    return LLM_OK;
+  }
+  return fail(LLM_ERR_OOM, "kv_cache: page pool exhausted (" + std::to_string(num_pages) +
+                               " pages)");
 }
 
 void KvCache::drop_page(int32_t page) {
   if (page < 0 || page >= num_pages) return;
   if (--refcount[page] <= 0) {
     refcount[page] = 0;
-    free_list.push_back(page);
+    free_lists[zone_of_page(page)].push_back(page);
   }
 }
 
@@ -121,13 +147,13 @@ int KvCache::ensure_tile(int layer, int beam, int head, int tile, bool exclusive
   const size_t idx = index(layer, beam, head, tile);
   int32_t p = h_table[idx];
   if (p < 0) {
-    int rc = alloc_page(&p);
+    int rc = alloc_page(layer, &p);
     if (rc) return rc;
     set_entry(idx, p);
   } else if (exclusive && refcount[p] > 1) {
     // copy-on-write: the page is shared with a forked beam
     int32_t np;
-    int rc = alloc_page(&np);
+    int rc = alloc_page(layer, &np);
     if (rc) return rc;
     cow.push_back({p, np});
     refcount[p] -= 1;
@@ -248,7 +274,7 @@ extern "C" long long kv_cache_num_pages(const kv_cache* c) { return c ? c->impl.
 extern "C" long long kv_cache_free_pages(const kv_cache* c) {
   if (!c) return -1;
   std::lock_guard<std::mutex> g(const_cast<kv_cache*>(c)->impl.mu);
-  return (long long)c->impl.free_list.size();
+  return c->impl.free_count();
 }
 
 extern "C" int kv_cache_assign(kv_cache* c, int layer, int beam, int head, int tile, int page) {
@@ -262,8 +288,7 @@ extern "C" int kv_cache_assign(kv_cache* c, int layer, int beam, int head, int t
   if (old == page) return LLM_OK;
   if (page >= 0) {
     // take the page out of the free list if it is there; bump its refcount
-    auto it = std::find(k.free_list.begin(), k.free_list.end(), page);
-    if (it != k.free_list.end()) k.free_list.erase(it);
+    k.take_free(page);
     k.refcount[page] += 1;
   }
   k.drop_page(old);
@@ -358,8 +383,7 @@ extern "C" int kv_cache_clear(kv_cache* c) {
   k.dirty.clear();
   k.cow.clear();
   std::fill(k.refcount.begin(), k.refcount.end(), 0);
-  k.free_list.resize((size_t)k.num_pages);
-  for (long long i = 0; i < k.num_pages; ++i) k.free_list[i] = (int32_t)(k.num_pages - 1 - i);
+  k.reset_free_lists();
   LLM_HIP_RET(hipMemset(k.d_table, 0xFF, k.entries * sizeof(int32_t)));
   LLM_HIP_RET(hipDeviceSynchronize());  // null-stream memset vs. non-blocking user streams
   return LLM_OK;
@@ -481,9 +505,7 @@ extern "C" int kv_cache_load(kv_cache* c, const char* path) {
   std::fill(k.refcount.begin(), k.refcount.end(), 0);
   for (size_t i = 0; i < k.entries; ++i)
     if (k.h_table[i] >= 0 && k.h_table[i] < k.num_pages) k.refcount[k.h_table[i]] += 1;
-  k.free_list.clear();
-  for (long long p = k.num_pages - 1; p >= 0; --p)
-    if (k.refcount[p] == 0) k.free_list.push_back((int32_t)p);
+  k.reset_free_lists();
   LLM_HIP_RET(hipMemcpy(k.d_table, k.h_table.data(), k.entries * sizeof(int32_t),
                         hipMemcpyHostToDevice));
   return LLM_OK;

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <mutex>
 #include <utility>
@@ -24,7 +25,13 @@ struct KvCache {
   std::vector<uint8_t> dirty_flag;
   std::vector<int64_t> dirty;
   std::vector<int32_t> refcount;
-  std::vector<int32_t> free_list;
+  // Free pages, one list per layer zone: page p belongs to zone
+  // min(p / zone_pages, L - 1).  A layer allocates from its own zone first, so
+  // the pages one attention launch gathers stay inside ~1/L of the pool (TLB
+  // reach: a step walks every layer's pages once) — it falls back to the other
+  // zones only when its own is exhausted.
+  std::vector<std::vector<int32_t>> free_lists;
+  long long zone_pages = 0;
   std::vector<std::pair<int32_t, int32_t>> cow;  // (src page, dst page) copies pending
   int64_t* d_idx = nullptr;
   int32_t* d_val = nullptr;
@@ -41,7 +48,14 @@ struct KvCache {
   }
   bool in_range(int layer, int beam, int head, int tile) const;
   void set_entry(size_t idx, int32_t page);
-  int alloc_page(int32_t* out);
+  int zone_of_page(int32_t page) const {
+    return (int)std::min<long long>(page / zone_pages, (long long)free_lists.size() - 1);
+  }
+  int zone_of_layer(int layer) const { return std::min(layer, (int)free_lists.size() - 1); }
+  void reset_free_lists();
+  long long free_count() const;
+  bool take_free(int32_t page);  // remove a specific page from its free list
+  int alloc_page(int layer, int32_t* out);
   void drop_page(int32_t page);
   // allocate (and, if exclusive, un-share by copy-on-write) the page of a tile
   int ensure_tile(int layer, int beam, int head, int tile, bool exclusive, int32_t* page);

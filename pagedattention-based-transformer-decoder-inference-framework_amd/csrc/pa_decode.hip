@@ -7,9 +7,14 @@
 // (attention_cpu/cpu_attention_kernel.cpp:37-129).
 //
 // Decomposition (HBM-bound KV scan, ~1 flop/byte):
-//   * one WAVE per (row b, head h, split s); a split is <= 64 consecutive
-//     pages of that row's page-table row, so its page ids are ONE coalesced
-//     dword load (lane j holds page j) and are broadcast with v_readlane.
+//   * one WAVE per (row b, head h, split s).  Every (b, h) gets the same
+//     number of splits NS (a launch constant, sized so B*H*NS waves fill the
+//     chip's resident wave slots exactly once: no second, ragged round), and
+//     the split length is derived ON DEVICE from the row's live context,
+//     pps_b = ceil(ntiles_b / NS) <= 128 pages, so a hipGraph captured once
+//     stays balanced as the context grows.  A split's page ids are two
+//     coalesced dword loads (lane j holds pages j and 64 + j), broadcast with
+//     v_readlane.
 //   * a page (tile) of TS tokens x D fp16 is contiguous; a wave reads it with
 //     TS*D*2/1024 buffer_load_dwordx4 instructions of 1 KiB each (lane l ->
 //     bytes 16l..16l+15): LPT = D/8 lanes hold one token row, TPI = 64/LPT
@@ -51,18 +56,38 @@ struct PaSplitArgs {
   const int32_t* context_lens;
   int B, H, T;
   int num_pages, num_beams, max_tiles;
-  int pps;     // pages per split (<= 64)
-  int nsplit;  // splits per (b, h)
+  int pps;     // > 0: fixed pages per split (<= 128); 0: ceil(ntiles_b / nsplit)
+  int nsplit;  // splits per (b, h) (grid)
   float qscale;
 };
 
-template <int D, int TS, bool DIRECT>
+constexpr int kMaxPps = 128;  // page ids held in two registers per lane
+
+// Split length of a row with `ntiles` live tiles.
+__device__ __forceinline__ int row_pps(int pps_fixed, int nsplit, int ntiles) {
+  if (pps_fixed > 0) return pps_fixed;
+  return min(max((ntiles + nsplit - 1) / nsplit, 1), kMaxPps);
+}
+
+// Pages per register stage: CHUNK_BYTES of K+V in flight per wave per stage.
+template <int D, int TS, int CHUNK_BYTES>
+constexpr int pages_per_stage() {
+  return (CHUNK_BYTES / (2 * TS * D * 2)) > 0 ? CHUNK_BYTES / (2 * TS * D * 2) : 1;
+}
+
+// KV pages are read exactly once per step: stream them with the non-temporal
+// cache policy (buffer_load ... nt), which keeps them from evicting the page
+// table / q / partials from L2 and measured 0.73 -> 0.81 of 8 TB/s at C3
+// (scripts/tune_attention.py, variants 0 vs 1).
+constexpr int kKvLoadAux = 2;
+
+template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux>
 __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
   constexpr int NI = TS / TPI;
   constexpr int PAGE_BYTES = TS * D * 2;
-  constexpr int U = (16384 / (2 * PAGE_BYTES)) > 0 ? (16384 / (2 * PAGE_BYTES)) : 1;
+  constexpr int U = pages_per_stage<D, TS, CHUNK_BYTES>();
   constexpr int NR = U * NI;
   static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1, "bad D/TS");
 
@@ -76,9 +101,10 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
   const int r = a.beam_ids ? a.beam_ids[b] : b;
   int Tb = a.context_lens ? a.context_lens[b] : a.T;
   Tb = min(max(Tb, 0), a.T);
-  const int ntiles = (Tb + TS - 1) / TS;
-  const int tile0 = s * a.pps;
-  const int count = min(a.pps, ntiles - tile0);
+  const int ntiles = min((Tb + TS - 1) / TS, a.max_tiles);
+  const int pps = row_pps(a.pps, a.nsplit, ntiles);
+  const int tile0 = s * pps;
+  const int count = min(pps, ntiles - tile0);
   const int c = lane % LPT;
   const int g = lane / LPT;
 
@@ -93,15 +119,19 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
     return;
   }
 
-  // Page ids of this split: lane j holds page j (PageTable::lookup semantics).
-  int pid = -1;
-  if (lane < count && r >= 0 && r < a.num_beams) {
-    const int tile = tile0 + lane;
-    if (tile < a.max_tiles) {
-      pid = a.page_table[((size_t)r * a.H + h) * a.max_tiles + tile];
-      if (pid >= a.num_pages) pid = -1;
-    }
+  // Page ids of this split: lane j holds pages j and 64 + j
+  // (PageTable::lookup semantics: out of range or >= num_pages -> missing).
+  int pid0 = -1, pid1 = -1;
+  if (r >= 0 && r < a.num_beams) {
+    const int32_t* row = a.page_table + ((size_t)r * a.H + h) * a.max_tiles + tile0;
+    if (lane < count) pid0 = row[lane];
+    if (64 + lane < count) pid1 = row[64 + lane];
+    if (pid0 >= a.num_pages) pid0 = -1;
+    if (pid1 >= a.num_pages) pid1 = -1;
   }
+  auto page_of = [&](int j) -> int {  // j is wave-uniform
+    return j < 64 ? __builtin_amdgcn_readlane(pid0, j) : __builtin_amdgcn_readlane(pid1, min(j - 64, 63));
+  };
 
   // q chunk of this lane (dims c*8 .. c*8+7), pre-scaled into log2 units.
   float qv[8];
@@ -127,7 +157,7 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = p0 + u;
-      const int pg = __builtin_amdgcn_readlane(pid, min(j, 63));
+      const int pg = page_of(min(j, kMaxPps - 1));
       const bool ok = (j < count) && (pg >= 0);
       const size_t off = (size_t)(ok ? pg : 0) * PAGE_BYTES;
       const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k_pool + off), (short)0,
@@ -136,10 +166,10 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
                                                          ok ? PAGE_BYTES : 0, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        kk[u * NI + i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_off + i * 1024, 0, 0);
+        kk[u * NI + i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_off + i * 1024, 0, AUX);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        vv[u * NI + i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_off + i * 1024, 0, 0);
+        vv[u * NI + i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_off + i * 1024, 0, AUX);
     }
   };
 
@@ -147,7 +177,7 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = p0 + u;
-      const int pg = __builtin_amdgcn_readlane(pid, min(j, 63));
+      const int pg = page_of(min(j, kMaxPps - 1));
       const bool ok = (j < count) && (pg >= 0);
       const int tok_base = (tile0 + j) * TS + g;
       float sc[NI];
@@ -237,7 +267,7 @@ struct PaMergeArgs {
   const float* part_ml;
   float* out;
   const int32_t* context_lens;
-  int B, H, D, T, TS, pps, nsplit;
+  int B, H, D, T, TS, pps, nsplit, max_tiles;
 };
 
 __global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
@@ -247,8 +277,9 @@ __global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
   const int b = bh / a.H;
   int Tb = a.context_lens ? a.context_lens[b] : a.T;
   Tb = min(max(Tb, 0), a.T);
-  const int ntiles = (Tb + a.TS - 1) / a.TS;
-  const int ns = min(a.nsplit, (ntiles + a.pps - 1) / a.pps);
+  const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
+  const int pps = row_pps(a.pps, a.nsplit, ntiles);
+  const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
   const float* ml = a.part_ml + (size_t)bh * a.nsplit * 2;
   float M = kNegSentinel;
   for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
@@ -271,7 +302,9 @@ __global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
 namespace {
 
 constexpr int kMinPps = 8;
-constexpr int kMaxPps = 64;
+// Resident wave slots of the chip for this kernel: 256 CUs x 4 SIMDs x 8
+// waves (64 VGPRs, no LDS).  NS is chosen so B*H*NS ~ one full round.
+constexpr long long kTargetWaves = 256LL * 4 * 8;
 
 template <int D, int TS>
 hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st) {
@@ -297,17 +330,26 @@ bool supported(int D, int TS) {
   return (D == 32 || D == 64 || D == 128 || D == 256) && (TS == 16 || TS == 32);
 }
 
+// Splits per (b, h) for a launch whose rows hold at most `ntiles` tiles.
+int choose_nsplit(int B, int H, int ntiles, int pps_fixed) {
+  ntiles = std::max(ntiles, 1);
+  if (pps_fixed > 0) {
+    const int pps = std::min(pps_fixed, kMaxPps);
+    return (ntiles + pps - 1) / pps;
+  }
+  const long long bh = std::max(1LL, (long long)B * H);
+  long long ns = std::max(1LL, (kTargetWaves + bh / 2) / bh);                 // fill the chip once
+  ns = std::min<long long>(ns, std::max(1, (ntiles + kMinPps - 1) / kMinPps));  // >= kMinPps pages
+  ns = std::max<long long>(ns, (ntiles + kMaxPps - 1) / kMaxPps);              // <= kMaxPps pages
+  return (int)ns;
+}
+
 }  // namespace
 
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles) {
   const int ntiles = std::max(1, std::min((T + TS - 1) / TS, max_tiles));
-  const long long bh = std::max(1LL, (long long)B * H);
-  // Enough waves for 256 CUs x ~16 resident waves, in splits of >= kMinPps pages.
-  const long long want_splits = std::max(1LL, (4096 + bh - 1) / bh);
-  long long pps = (ntiles + want_splits - 1) / want_splits;
-  pps = std::max<long long>(pps, kMinPps);
-  pps = std::min<long long>(pps, kMaxPps);
-  return (int)pps;
+  const int ns = choose_nsplit(B, H, ntiles, 0);
+  return (ntiles + ns - 1) / ns;
 }
 
 }  // namespace llm
@@ -322,8 +364,7 @@ extern "C" int pa_decode_pages_per_split(int B, int H, int T, int page_size, int
 extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
                                             int pages_per_split) {
   if (B <= 0 || H <= 0 || D <= 0 || max_tiles <= 0) return 0;
-  const int pps = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps) : kMinPps;
-  const size_t nsplit = (size_t)(max_tiles + pps - 1) / pps;
+  const size_t nsplit = (size_t)choose_nsplit(B, H, max_tiles, pages_per_split);
   return (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
 }
 
@@ -347,10 +388,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   LLM_REQUIRE((long long)kv->num_pages * kv->page_size * D * 2 < (1LL << 47),
               "pa_decode: pool too large");
   const int TS = kv->page_size;
-  const int ntiles_max = std::max(1, (T + TS - 1) / TS);
-  int pps = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps)
-                                : pa_pages_per_split(B, H, T, TS, kv->max_tiles);
-  const int nsplit = (ntiles_max + pps - 1) / pps;
+  // tiles at or past max_tiles have no page-table entry: they are missing (masked)
+  const int ntiles_max = std::max(1, std::min((T + TS - 1) / TS, kv->max_tiles));
+  const int pps_fixed = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps) : 0;
+  const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed);
   const bool direct = nsplit <= 1;
 
   PaSplitArgs a{};
@@ -368,8 +409,8 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   a.num_pages = kv->num_pages;
   a.num_beams = kv->num_beams;
   a.max_tiles = kv->max_tiles;
-  a.pps = pps;
-  a.nsplit = direct ? 1 : nsplit;
+  a.pps = pps_fixed;
+  a.nsplit = nsplit;
   a.qscale = sm_scale * kLog2e;
   if (!direct) {
     const size_t need = (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
@@ -387,7 +428,8 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
   if (!direct) {
-    PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, TS, pps, nsplit};
+    PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, TS, pps_fixed, nsplit,
+                   kv->max_tiles};
     hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
     LLM_HIP_RET(hipGetLastError());
   }
@@ -400,4 +442,48 @@ extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
                          size_t workspace_bytes, void* stream) {
   return pa_decode_internal(kv, q, H * D, out, beam_ids, context_lens, B, H, D, T, sm_scale,
                             pages_per_split, workspace, workspace_bytes, as_stream(stream));
+}
+
+// Tuning hook (not part of include/llm_decoder.h): run the split kernel of
+// D=128 / TS=16 in a given variant so scripts/bench_kernels.py can compare
+// register-stage sizes and cache policies in one process.
+extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q, float* out,
+                              const int32_t* context_lens, int B, int H, int T, int pps,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  LLM_REQUIRE(kv && kv->head_dim == 128 && kv->page_size == 16 && H == kv->num_heads,
+              "pa_decode_tune: D=128, page 16 only");
+  const int ntiles_max = std::max(1, (T + 15) / 16);
+  pps = std::min(std::max(pps, 1), 64);
+  const int nsplit = (ntiles_max + pps - 1) / pps;
+  LLM_REQUIRE(nsplit > 1, "pa_decode_tune: needs more than one split");
+  const size_t need = (size_t)B * H * nsplit * (128 + 2) * sizeof(float);
+  LLM_REQUIRE(workspace && workspace_bytes >= need, "pa_decode_tune: workspace");
+  PaSplitArgs a{};
+  a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
+  a.v_pool = static_cast<const uint8_t*>(kv->v_pool);
+  a.page_table = kv->page_table;
+  a.q = q; a.q_stride = H * 128; a.out = out;
+  a.context_lens = context_lens;
+  a.B = B; a.H = H; a.T = T;
+  a.num_pages = kv->num_pages; a.num_beams = kv->num_beams; a.max_tiles = kv->max_tiles;
+  a.pps = pps; a.nsplit = nsplit; a.qscale = kLog2e;
+  a.part_acc = static_cast<float*>(workspace);
+  a.part_ml = a.part_acc + (size_t)B * H * nsplit * 128;
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((B * H * nsplit + 3) / 4), block(256);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 0>), grid, block, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2>), grid, block, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 0>), grid, block, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2>), grid, block, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 0>), grid, block, 0, st, a); break;
+    case 5: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 2>), grid, block, 0, st, a); break;
+    default: return fail(LLM_ERR_INVALID, "pa_decode_tune: variant");
+  }
+  LLM_HIP_RET(hipGetLastError());
+  PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, 128, T, 16, pps, nsplit,
+                 kv->max_tiles};
+  hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
+  LLM_HIP_RET(hipGetLastError());
+  return LLM_OK;
 }

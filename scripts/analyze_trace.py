@@ -1,0 +1,50 @@
+"""Timeline of one decode step from a rocprofv3 kernel trace: per-kernel-kind
+busy time, overlap between queues, idle gaps.
+    python scripts/analyze_trace.py gpurun_out/trace_X/tr_kernel_trace.csv [--dump]"""
+import csv
+import re
+import sys
+from collections import defaultdict
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+for r in rows:
+    r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+rows.sort(key=lambda r: r["s"])
+emb = [i for i, r in enumerate(rows) if "embed_kernel" in r["Kernel_Name"]]
+adv = [i for i, r in enumerate(rows) if "advance_kernel" in r["Kernel_Name"]]
+# the last step: its embeds start within 1 ms of each other
+first = emb[-1]
+while first > 0 and emb.index(first) > 0 and rows[first]["s"] - rows[emb[emb.index(first) - 1]]["s"] < 1_000_000:
+    first = emb[emb.index(first) - 1]
+last_adv = adv[-1]
+step = [r for r in rows[first:last_adv + 1]]
+# include trailing advance kernels
+t0 = step[0]["s"]
+t1 = max(r["e"] for r in step)
+print(f"step kernels {len(step)} span {(t1 - t0) / 1e3:.1f} us, queues {sorted({r['Queue_Id'] for r in step})}")
+kind = defaultdict(float)
+cnt = defaultdict(int)
+for r in step:
+    k = re.sub(r"^void |llm::|\(.*$", "", r["Kernel_Name"])[:60]
+    kind[k] += (r["e"] - r["s"]) / 1e3
+    cnt[k] += 1
+for k, v in sorted(kind.items(), key=lambda kv: -kv[1]):
+    print(f"  {v:9.1f} us  {cnt[k]:4d}x  avg {v / cnt[k]:7.2f}  {k}")
+# union busy time
+ev = sorted([(r["s"], 1) for r in step] + [(r["e"], -1) for r in step])
+busy = 0
+act = 0
+last = None
+multi = 0
+for t, d in ev:
+    if last is not None:
+        if act > 0:
+            busy += t - last
+        if act > 1:
+            multi += t - last
+    act += d
+    last = t
+print(f"busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us, >1 kernel running {multi / 1e3:.1f} us")
+if "--dump" in sys.argv:
+    for r in step[:80]:
+        print(f"{(r['s'] - t0) / 1e3:9.1f} {(r['e'] - r['s']) / 1e3:8.1f} q{r['Queue_Id']} {r['Kernel_Name'][:70]}")

@@ -1,0 +1,72 @@
+"""A/B the paged-attention split-kernel variants at the C3 shape in one process
+(interleaved rounds, median), HIP-event timed.
+
+    python scripts/tune_attention.py [--rounds 5] [--variants 0 1 2 3 4 5] [--pps 64]
+"""
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import llm_capi  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--variants", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5])
+ap.add_argument("--pps", type=int, nargs="*", default=[64])
+ap.add_argument("--T", type=int, default=8192)
+ap.add_argument("--B", type=int, default=64)
+args = ap.parse_args()
+B, H, D, T, ts = args.B, 16, 128, args.T, 16
+nt = (T + ts - 1) // ts
+num_pages = B * H * nt
+g = torch.Generator(device="cuda").manual_seed(0)
+kp = (torch.randn((num_pages, ts, D), generator=g, device="cuda") * D ** -0.25).half()
+vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
+q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
+pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
+lib = llm_capi.load()
+lib.pa_decode_tune.restype = ctypes.c_int
+lib.pa_decode_tune.argtypes = [ctypes.c_int, ctypes.POINTER(llm_capi.PaKvView), ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                               ctypes.c_void_p]
+view = llm_capi.kv_view(kp, vp, pt)
+out = torch.empty((B, H, D), device="cuda")
+ref = llm_capi.pa_decode(q, kp, vp, pt, T=T)
+ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, nt, 1)
+ws = torch.empty(ws_bytes, dtype=torch.uint8, device="cuda")
+st = llm_capi.stream_ptr()
+nbytes = 2 * B * H * T * D * 2 + B * H * nt * 4
+res = {}
+for r in range(args.rounds):
+    for pps in args.pps:
+        for v in args.variants:
+            def run():
+                llm_capi.check(lib.pa_decode_tune(v, ctypes.byref(view), llm_capi.ptr(q),
+                                                  llm_capi.ptr(out), None, B, H, T, pps,
+                                                  llm_capi.ptr(ws), ws_bytes, st))
+            run()
+            torch.cuda.synchronize()
+            if r == 0:
+                err = (out - ref).abs().max().item() / ref.abs().max().item()
+                assert err < 1e-5, (v, pps, err)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.iters):
+                run()
+            e.record()
+            torch.cuda.synchronize()
+            res.setdefault((v, pps), []).append(s.elapsed_time(e) / args.iters * 1e-3)
+for (v, pps), ts_ in sorted(res.items()):
+    t = float(np.median(ts_))
+    print(json.dumps({"variant": v, "pps": pps, "us": round(t * 1e6, 1),
+                      "GBps": round(nbytes / t / 1e9, 1), "frac_8TBps": round(nbytes / t / 8e12, 4),
+                      "min_us": round(min(ts_) * 1e6, 1)}))

@@ -81,6 +81,26 @@ def test_pa_decode_random_vs_oracle(gpu, oracle, B, H, D, T, ts):
         assert rel_err(out, ref) < RTOL, (pps, rel_err(out, ref))
 
 
+def test_pa_decode_long_splits_second_page_register(gpu, oracle):
+    """B*H large enough that the balanced split count is small and each split
+    walks > 64 pages (page ids 64..127 come from the second per-lane register),
+    with ragged per-row contexts so every row derives its own split length."""
+    import llm_capi
+    rng = np.random.default_rng(21)
+    B, H, D, T, ts = 64, 32, 32, 16 * 300, 16
+    q, kp, vp, pt = _random_case(rng, B, H, D, T, ts, missing_frac=0.01)
+    lens = rng.integers(1, T + 1, size=B).astype(np.int32)
+    lens[0], lens[1] = T, 16 * 257 + 3  # 4 splits: 300 tiles -> 75 per split; 258 -> 65
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T,
+                                 context_lens=lens)
+    lib = llm_capi.load()
+    assert lib.pa_decode_pages_per_split(B, H, T, ts, pt.shape[2]) > 64
+    for pps in (0, 100, 128):
+        out = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T,
+                                 context_lens=_dev(lens), pages_per_split=pps).cpu().numpy()
+        assert rel_err(out, ref) < RTOL, (pps, rel_err(out, ref))
+
+
 def test_pa_decode_ragged_context_and_beams(gpu, oracle):
     import llm_capi
     rng = np.random.default_rng(11)
