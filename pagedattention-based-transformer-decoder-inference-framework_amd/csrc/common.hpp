@@ -80,4 +80,17 @@ __device__ __forceinline__ int wave_id_uniform() {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+// Offset of activation element (m, k) in MFMA A-fragment order ("packed A"):
+// one contiguous 1 KiB block per (16-row tile, k-step), lane l of the block
+// holding row l&15 and 16 B of k (16 int8 or 8 fp16) — the exact operand
+// layout of v_mfma_i32_16x16x64_i8 / v_mfma_f32_16x16x32_f16, so the GEMM
+// reads each fragment with one coalesced buffer_load_dwordx4.
+// KS = k-steps per row (K/64 for int8, K/32 for fp16).  Offsets in elements.
+__host__ __device__ __forceinline__ size_t a_frag_off_i8(int m, int k, int KS) {
+  return ((size_t)((m >> 4) * KS + (k >> 6)) * 64 + (m & 15) + 16 * ((k & 63) >> 4)) * 16 + (k & 15);
+}
+__host__ __device__ __forceinline__ size_t a_frag_off_f16(int m, int k, int KS) {
+  return ((size_t)((m >> 4) * KS + (k >> 5)) * 64 + (m & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+}
+
 }  // namespace llm

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "gemm.hpp"
 #include "kv_cache_impl.hpp"
 #include "pa_decode.hpp"
 #include "row_ops.hpp"
@@ -143,9 +144,9 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   if (c.max_batch <= 0) c.max_batch = 1;
   if (c.attn_scale == 0.f) c.attn_scale = 1.f;
   RET_IF(check_cfg(c));
-  const int kstep = c.weight_dtype == LLM_I8 ? 64 : 32;
-  LLM_REQUIRE(c.hidden_dim % kstep == 0 && c.inter_dim % kstep == 0,
-              "decoder: hidden_dim and inter_dim must be multiples of 64 (int8) / 32 (fp16)");
+  LLM_REQUIRE(c.hidden_dim % 64 == 0 && c.inter_dim % 64 == 0 && c.inter_dim <= 16384,
+              "decoder: hidden_dim and inter_dim must be multiples of 64 (packed GEMM "
+              "activations), inter_dim <= 16384");
   std::unique_ptr<llm_decoder> d(new llm_decoder());
   d->cfg = c;
   d->L = c.num_layers; d->H = c.num_heads; d->D = c.head_dim; d->hid = c.hidden_dim;
@@ -164,8 +165,9 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->h1.alloc((size_t)B * inter));
   RET_IF(d->logits.alloc((size_t)B * d->V));
   RET_IF(d->sa.alloc((size_t)B));
-  RET_IF(d->qa.alloc((size_t)B * std::max(hid, inter)));
-  if (d->wdtype == LLM_F16) RET_IF(d->a16.alloc((size_t)B * std::max(hid, inter)));
+  const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
+  RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
+  if (d->wdtype == LLM_F16) RET_IF(d->a16.alloc(B16 * std::max(hid, inter)));
   RET_IF(d->tokens.alloc((size_t)B));
   RET_IF(d->pos.alloc((size_t)B));
   RET_IF(d->ctx.alloc((size_t)B));
@@ -298,31 +300,41 @@ struct MicroBatch {
   uint8_t* attn_ws = nullptr;
 };
 
+// Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
+// order (common.hpp a_frag_off_*): their producers (LayerNorm+quant, the
+// attention merge, the row quantiser) write MFMA A-fragments directly, so
+// every GEMM A load is one coalesced 1 KiB read.  Micro-batches start on
+// 16-row boundaries, so a row offset r0 is the same base offset in both
+// layouts (r0 * K elements).
 int llm_decoder::layer_pre(int l, hipStream_t st, const MicroBatch& mb) {
   const int r0 = mb.r0, B = mb.n;
   const size_t lh = (size_t)l * hid;
   float* xr = x.p + (size_t)r0 * hid;
-  float* qkvr = qkv.p + (size_t)r0 * 3 * hid;
+  float* qr = qkv.p + (size_t)r0 * hid;  // q only: K and V go straight into the pages
+  pa_kv_view view;
+  RET_IF(kv_cache_view(kv, l, &view));
+  const KvAppendView app{pos.p + r0, view.page_table + (size_t)r0 * H * view.max_tiles,
+                         kv_cache_k_pool(kv), kv_cache_v_pool(kv), view.num_beams - r0,
+                         view.max_tiles, TS, view.num_pages, H, D};
+  WeightGemm g;
+  g.dtype = wdtype;
+  g.a_packed = 1;
+  g.W_packed = wqkv.p + sz_qkv * l;
+  g.M = B; g.N = 3 * hid; g.K = hid;
+  g.C = qr; g.c_cols = hid; g.c_ld = hid;
+  g.kv = &app;
   if (wdtype == LLM_I8) {
     int8_t* qar = qa.p + (size_t)r0 * qa_ld;
     float* sar = sa.p + r0;
     LLM_HIP_RET(launch_layernorm_quant(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
-                                       qar, sar, st));
-    RET_IF(i8_gemm(qar, hid, wqkv.p + sz_qkv * l, nullptr, qkvr, B, 3 * hid, hid, sar,
-                   sw_qkv.p + (size_t)l * 3 * hid, nullptr, LLM_ACT_NONE, st));
+                                       qar, sar, st, 1));
+    g.A = qar; g.sa = sar; g.sw = sw_qkv.p + (size_t)l * 3 * hid;
   } else {
     uint16_t* a16r = a16.p + (size_t)r0 * qa_ld;
-    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, a16r, st));
-    RET_IF(f16_gemm(a16r, hid, wqkv.p + sz_qkv * l, qkvr, B, 3 * hid, hid, nullptr, LLM_ACT_NONE,
-                    st));
+    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, a16r, st, 1));
+    g.A = a16r;
   }
-  pa_kv_view view;
-  RET_IF(kv_cache_view(kv, l, &view));
-  LLM_HIP_RET(launch_kv_append(qkvr, B, H, D, pos.p + r0,
-                               view.page_table + (size_t)r0 * H * view.max_tiles,
-                               view.num_beams - r0, view.max_tiles, TS, view.num_pages,
-                               kv_cache_k_pool(kv), kv_cache_v_pool(kv), st));
-  return LLM_OK;
+  return weight_gemm(g, st);
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const MicroBatch& mb) {
@@ -331,41 +343,56 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const MicroBatch& mb) {
   RET_IF(kv_cache_view(kv, l, &view));
   view.page_table += (size_t)r0 * H * view.max_tiles;  // rows of this micro-batch
   view.num_beams -= r0;
-  return pa_decode_internal(&view, qkv.p + (size_t)r0 * 3 * hid, 3 * hid, o.p + (size_t)r0 * hid,
-                            nullptr, ctx.p + r0, B, H, D, cfg.max_seq_len, cfg.attn_scale, pps,
-                            mb.attn_ws, attn_ws_bytes, st);
+  // the split merge also produces the o_proj input (packed int8 + scale, or fp16)
+  PaRowOutputs ro;
+  ro.pack = 1;
+  if (wdtype == LLM_I8) {
+    ro.q = qa.p + (size_t)r0 * qa_ld;
+    ro.inv_scale = sa.p + r0;
+  } else {
+    ro.out16 = a16.p + (size_t)r0 * qa_ld;
+  }
+  return pa_decode_internal(&view, qkv.p + (size_t)r0 * hid, hid, o.p + (size_t)r0 * hid, nullptr,
+                            ctx.p + r0, B, H, D, cfg.max_seq_len, cfg.attn_scale, pps, mb.attn_ws,
+                            attn_ws_bytes, st, &ro);
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const MicroBatch& mb) {
   const int r0 = mb.r0, B = mb.n;
   const size_t lh = (size_t)l * hid;
   float* xr = x.p + (size_t)r0 * hid;
-  float* orow = o.p + (size_t)r0 * hid;
   float* h1r = h1.p + (size_t)r0 * inter;
-  if (wdtype == LLM_I8) {
-    int8_t* qar = qa.p + (size_t)r0 * qa_ld;
-    float* sar = sa.p + r0;
-    LLM_HIP_RET(launch_quantize_rows(orow, B, hid, qar, sar, st));
-    RET_IF(i8_gemm(qar, hid, wo.p + sz_o * l, nullptr, xr, B, hid, hid, sar, sw_o.p + lh, nullptr,
-                   LLM_ACT_NONE, st));
+  const bool i8 = wdtype == LLM_I8;
+  void* ar = i8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
+  float* sar = sa.p + r0;
+  WeightGemm g;
+  g.dtype = wdtype;
+  g.a_packed = 1;
+  g.A = ar;
+  g.M = B;
+  // o_proj: input produced (packed) by the attention merge
+  g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = xr;
+  if (i8) { g.sa = sar; g.sw = sw_o.p + lh; }
+  RET_IF(weight_gemm(g, st));
+  // LN2 -> mlp_fc1 (+b1, ReLU)
+  if (i8)
     LLM_HIP_RET(launch_layernorm_quant(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
-                                       qar, sar, st));
-    RET_IF(i8_gemm(qar, hid, w1.p + sz_1 * l, nullptr, h1r, B, inter, hid, sar,
-                   sw1.p + (size_t)l * inter, b1.p + (size_t)l * inter, LLM_ACT_RELU, st));
-    LLM_HIP_RET(launch_quantize_rows(h1r, B, inter, qar, sar, st));
-    RET_IF(i8_gemm(qar, inter, w2.p + sz_2 * l, nullptr, xr, B, hid, inter, sar, sw2.p + lh,
-                   b2.p + lh, LLM_ACT_NONE, st));
-  } else {
-    uint16_t* a16r = a16.p + (size_t)r0 * qa_ld;
-    LLM_HIP_RET(launch_to_f16(orow, (size_t)B * hid, a16r, st));
-    RET_IF(f16_gemm(a16r, hid, wo.p + sz_o * l, xr, B, hid, hid, nullptr, LLM_ACT_NONE, st));
-    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, a16r, st));
-    RET_IF(f16_gemm(a16r, hid, w1.p + sz_1 * l, h1r, B, inter, hid, b1.p + (size_t)l * inter,
-                    LLM_ACT_RELU, st));
-    LLM_HIP_RET(launch_to_f16(h1r, (size_t)B * inter, a16r, st));
-    RET_IF(f16_gemm(a16r, inter, w2.p + sz_2 * l, xr, B, hid, inter, b2.p + lh, LLM_ACT_NONE, st));
-  }
-  return LLM_OK;
+                                       static_cast<int8_t*>(ar), sar, st, 1));
+  else
+    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, ar, st, 1));
+  g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid; g.C = h1r;
+  g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
+  if (i8) g.sw = sw1.p + (size_t)l * inter;
+  RET_IF(weight_gemm(g, st));
+  // quantise h1 -> mlp_fc2 (+b2)
+  if (i8)
+    LLM_HIP_RET(launch_quantize_rows(h1r, B, inter, static_cast<int8_t*>(ar), sar, st, 1));
+  else
+    LLM_HIP_RET(launch_to_f16(h1r, (size_t)B * inter, ar, st, inter));
+  g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = xr;
+  g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
+  if (i8) g.sw = sw2.p + lh;
+  return weight_gemm(g, st);
 }
 
 int llm_decoder::step_head(hipStream_t st, const MicroBatch& mb) {
@@ -403,7 +430,17 @@ int llm_decoder::enqueue_step(hipStream_t st) {
     }
     return step_tail(st, mbs[0]);
   }
-  const int h0 = (batch + 1) / 2;
+  const int h0 = ((batch + 1) / 2 + 15) / 16 * 16;  // packed-A tiles are 16 rows
+  if (h0 >= batch) {
+    mbs[0] = {0, batch, attn_ws.p};
+    RET_IF(step_head(st, mbs[0]));
+    for (int l = 0; l < L; ++l) {
+      RET_IF(layer_pre(l, st, mbs[0]));
+      RET_IF(layer_attn(l, st, mbs[0]));
+      RET_IF(layer_post(l, st, mbs[0]));
+    }
+    return step_tail(st, mbs[0]);
+  }
   mbs[0] = {0, h0, attn_ws.p};
   mbs[1] = {h0, batch - h0, attn_ws2.p};
   hipStream_t S[2] = {st, stream2};

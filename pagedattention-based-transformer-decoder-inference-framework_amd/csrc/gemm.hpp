@@ -1,0 +1,45 @@
+// Internal entries of csrc/gemm.hip used by the decoder runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "llm_decoder.h"
+
+namespace llm {
+
+// Where the fused qkv projection writes K and V: the pages of position pos[m]
+// of row m (page_table already offset to the first row of the launch).
+struct KvAppendView {
+  const int32_t* pos;
+  const int32_t* page_table;
+  void* k_pool;
+  void* v_pool;
+  int num_beams, max_tiles, page_size, num_pages, H, D;
+};
+
+// One decode weight GEMM (decoder-internal form of i8_gemm / f16_gemm):
+//   C[m, n] = act(acc[m, n] * sa[m] * sw[n] + bias[n])   (I8; F16 ignores sa/sw)
+// A row-major (lda) or packed-A (a_packed, see common.hpp a_frag_off_*); only
+// columns n < c_cols are stored to C (row stride c_ld); with kv != NULL the
+// columns [hid, 3 hid) are appended to the KV pages instead (qkv projection).
+struct WeightGemm {
+  int dtype = LLM_I8;
+  const void* A = nullptr;
+  int lda = 0;
+  int a_packed = 0;
+  const void* W_packed = nullptr;
+  int M = 0, N = 0, K = 0;
+  const float* sa = nullptr;
+  const float* sw = nullptr;
+  const float* bias = nullptr;
+  int act = LLM_ACT_NONE;
+  float* C = nullptr;
+  int c_cols = 0, c_ld = 0;  // 0: N
+  const KvAppendView* kv = nullptr;
+};
+
+int weight_gemm(const WeightGemm& g, hipStream_t st);
+
+}  // namespace llm

@@ -38,8 +38,10 @@
 //     every exponential is one v_exp_f32.
 #include "common.hpp"
 #include "pa_decode.hpp"
+#include "row_ops.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace llm {
 
@@ -81,8 +83,13 @@ constexpr int pages_per_stage() {
 // (scripts/tune_attention.py, variants 0 vs 1).
 constexpr int kKvLoadAux = 2;
 
-template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux>
-__global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
+// STAGES = register stages in flight per wave (2: the next chunk loads while
+// the current one is computed; 1: latency hidden by occupancy alone).
+// MIN_WAVES > 0 asks the compiler for that many waves per SIMD.
+template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
+          int STAGES = 2, int MIN_WAVES = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
+void pa_split_kernel(PaSplitArgs a) {
   constexpr int LPT = D / 8;
   constexpr int TPI = 64 / LPT;
   constexpr int NI = TS / TPI;
@@ -215,14 +222,22 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
   };
 
   const int nchunks = (count + U - 1) / U;
-  u32x4 kA[NR], vA[NR], kB[NR], vB[NR];
-  issue(kA, vA, 0);
-  for (int ch = 0; ch < nchunks; ch += 2) {
-    issue(kB, vB, (ch + 1) * U);  // past-the-end chunks load nothing (num_records 0)
-    compute(kA, vA, ch * U);
-    if (ch + 1 >= nchunks) break;
-    issue(kA, vA, (ch + 2) * U);
-    compute(kB, vB, (ch + 1) * U);
+  if constexpr (STAGES == 1) {
+    u32x4 kA[NR], vA[NR];
+    for (int ch = 0; ch < nchunks; ++ch) {
+      issue(kA, vA, ch * U);
+      compute(kA, vA, ch * U);
+    }
+  } else {
+    u32x4 kA[NR], vA[NR], kB[NR], vB[NR];
+    issue(kA, vA, 0);
+    for (int ch = 0; ch < nchunks; ch += 2) {
+      issue(kB, vB, (ch + 1) * U);  // past-the-end chunks load nothing (num_records 0)
+      compute(kA, vA, ch * U);
+      if (ch + 1 >= nchunks) break;
+      issue(kA, vA, (ch + 2) * U);
+      compute(kB, vB, (ch + 1) * U);
+    }
   }
 
   // Merge the TPI row groups of the wave (lanes with equal c).
@@ -261,6 +276,28 @@ __global__ __launch_bounds__(256) void pa_split_kernel(PaSplitArgs a) {
   }
 }
 
+// sum_s part[s * stride] * w_s over s < ns with w_s held by lane s (s < 64) /
+// lane s - 64 of w1: loads issued 8 splits at a time so a merge costs a few
+// memory round trips, not one per split; summation order s = 0, 1, ...
+__device__ __forceinline__ float merge_splits(const float* part, int stride, int ns, float w0,
+                                              float w1) {
+  float acc = 0.f;
+  for (int s0 = 0; s0 < ns; s0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = (s0 + u < ns) ? part[(size_t)(s0 + u) * stride] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int s2 = s0 + u;
+      if (s2 < ns) {
+        const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
+        acc += v[u] * ws;
+      }
+    }
+  }
+  return acc;
+}
+
 // Split merge (flash-decoding LSE combine): one wave per (b, h).
 struct PaMergeArgs {
   const float* part_acc;
@@ -292,19 +329,117 @@ __global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
   for (int s = 0; s < ns; ++s) L += ml[2 * s + 1] * __builtin_amdgcn_exp2f(ml[2 * s] - M);
   const float inv = 1.0f / (L + 1e-6f);
   const float* pa = a.part_acc + (size_t)bh * a.nsplit * a.D;
-  for (int d = lane; d < a.D; d += 64) {
-    float acc = 0.f;
-    for (int s = 0; s < ns; ++s) acc += pa[(size_t)s * a.D + d] * __builtin_amdgcn_exp2f(ml[2 * s] - M);
-    o[d] = acc * inv;
+  const float w0 = lane < ns ? __builtin_amdgcn_exp2f(ml[2 * lane] - M) : 0.f;
+  const float w1 = 64 + lane < ns ? __builtin_amdgcn_exp2f(ml[2 * (64 + lane)] - M) : 0.f;
+  for (int d = lane; d < a.D; d += 64) o[d] = merge_splits(pa + d, a.D, ns, w0, w1) * inv;
+}
+
+// Split merge fused with the next consumer's input conversion: one workgroup
+// per row b merges all H heads into an LDS row [H*D], then writes any of
+//   out   fp32 [B][H*D]            (pa_decode's output)
+//   q     int8 [B][H*D] + inv_scale[b]   (per-row quantisation of the o_proj
+//         input, int8_quant.cpp:5-13,59-64 — replaces a quantize_rows launch)
+//   out16 fp16 [B][H*D]            (fp16 o_proj input of the FP16 decoder)
+struct PaMergeRowArgs {
+  const float* part_acc;
+  const float* part_ml;
+  float* out;
+  int8_t* q;
+  float* inv_scale;
+  _Float16* out16;
+  const int32_t* context_lens;
+  int B, H, D, T, TS, pps, nsplit, max_tiles;
+  int pack;  // q / out16 in packed-A order (common.hpp a_frag_off_*)
+};
+
+__global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
+  extern __shared__ float row[];  // [H*D]
+  __shared__ float sh[16];
+  const int lane = lane_id();
+  const int w = wave_id_uniform();
+  const int nw = blockDim.x >> 6;
+  const int b = blockIdx.x;
+  const int hid = a.H * a.D;
+  int Tb = a.context_lens ? a.context_lens[b] : a.T;
+  Tb = min(max(Tb, 0), a.T);
+  const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
+  const int pps = row_pps(a.pps, a.nsplit, ntiles);
+  const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
+  for (int h = w; h < a.H; h += nw) {
+    const size_t bh = (size_t)b * a.H + h;
+    const float* ml = a.part_ml + bh * a.nsplit * 2;
+    // split weights, lane-parallel: lane holds splits lane and 64 + lane
+    const float m0 = lane < ns ? ml[2 * lane] : kNegSentinel;
+    const float m1 = 64 + lane < ns ? ml[2 * (64 + lane)] : kNegSentinel;
+    const float l0 = lane < ns ? ml[2 * lane + 1] : 0.f;
+    const float l1 = 64 + lane < ns ? ml[2 * (64 + lane) + 1] : 0.f;
+    const float M = wave_max(fmaxf(m0, m1));
+    float* dst = row + h * a.D;
+    if (ns <= 0 || M <= 0.5f * kNegSentinel) {
+      for (int d = lane; d < a.D; d += 64) dst[d] = 0.f;
+      continue;
+    }
+    const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
+    const float w1 = 64 + lane < ns ? __builtin_amdgcn_exp2f(m1 - M) : 0.f;
+    // same summation order as pa_merge_kernel: s = 0, 1, ... (sequential)
+    float L = 0.f;
+    for (int s2 = 0; s2 < ns; ++s2) {
+      const float ls = s2 < 64 ? __shfl(l0, s2, 64) : __shfl(l1, s2 - 64, 64);
+      const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
+      L += ls * ws;
+    }
+    const float inv = 1.0f / (L + 1e-6f);
+    const float* pa = a.part_acc + bh * a.nsplit * a.D;
+    for (int d = lane; d < a.D; d += 64) dst[d] = merge_splits(pa + d, a.D, ns, w0, w1) * inv;
   }
+  __syncthreads();
+  float am = 0.f;
+  for (int i = threadIdx.x; i < hid; i += blockDim.x) {
+    const float v = row[i];
+    am = fmaxf(am, fabsf(v));
+    if (a.out) a.out[(size_t)b * hid + i] = v;
+    if (a.out16)
+      a.out16[a.pack ? a_frag_off_f16(b, i, hid >> 5) : (size_t)b * hid + i] = (_Float16)v;
+  }
+  if (!a.q) return;
+  am = wave_max(am);
+  if (lane == 0) sh[w] = am;
+  __syncthreads();
+  am = sh[0];
+  for (int i = 1; i < nw; ++i) am = fmaxf(am, sh[i]);
+  const float scale = 127.f / (am + 1e-6f);
+  for (int i = threadIdx.x; i < hid; i += blockDim.x) {
+    float y = roundf(__fmul_rn(row[i], scale));
+    y = fminf(fmaxf(y, -128.f), 127.f);
+    a.q[a.pack ? a_frag_off_i8(b, i, hid >> 6) : (size_t)b * hid + i] = (int8_t)(int)y;
+  }
+  if (threadIdx.x == 0) a.inv_scale[b] = 1.0f / scale;
 }
 
 namespace {
 
 constexpr int kMinPps = 8;
-// Resident wave slots of the chip for this kernel: 256 CUs x 4 SIMDs x 8
-// waves (64 VGPRs, no LDS).  NS is chosen so B*H*NS ~ one full round.
-constexpr long long kTargetWaves = 256LL * 4 * 8;
+constexpr int kMaxWavesPerCu = 32;  // 8 per SIMD x 4 SIMDs (gfx950)
+
+// Resident waves of the whole chip for one split-kernel instantiation
+// (occupancy query x CU count), cached.  Fallback: 256 CUs x 3 waves/SIMD.
+template <int D, int TS, bool DIRECT>
+long long resident_waves() {
+  static long long cached = 0;
+  if (cached) return cached;
+  int dev = 0, cus = 0, blocks = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, pa_split_kernel<D, TS, DIRECT>, 256, 0) ==
+          hipSuccess &&
+      cus > 0 && blocks > 0) {
+    cached = (long long)cus * blocks * 4;
+  } else {
+    (void)hipGetLastError();
+    cached = 256LL * 4 * 3;
+  }
+  return cached;
+}
 
 template <int D, int TS>
 hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st) {
@@ -330,25 +465,61 @@ bool supported(int D, int TS) {
   return (D == 32 || D == 64 || D == 128 || D == 256) && (TS == 16 || TS == 32);
 }
 
-// Splits per (b, h) for a launch whose rows hold at most `ntiles` tiles.
-int choose_nsplit(int B, int H, int ntiles, int pps_fixed) {
+// Upper bound of the split count of any launch over rows of <= ntiles tiles
+// (workspace sizing; host-only, no device query).
+long long max_nsplit(int B, int H, int ntiles) {
+  ntiles = std::max(ntiles, 1);
+  const long long bh = std::max(1LL, (long long)B * H);
+  const long long cap = 256LL * kMaxWavesPerCu;  // largest resident-wave count
+  const long long lo = (ntiles + kMaxPps - 1) / kMaxPps;
+  return std::max(lo, std::min<long long>((ntiles + kMinPps - 1) / kMinPps, lo + (cap + bh - 1) / bh + 1));
+}
+
+// Splits per (b, h): the smallest NS that is a whole number of resident-wave
+// rounds (B*H*NS ~ k * resident) with splits of <= kMaxPps pages, so every wave
+// carries the same page count and the last round is not a ragged tail; never
+// below kMinPps pages per split.
+int choose_nsplit(int B, int H, int ntiles, int pps_fixed, long long resident) {
   ntiles = std::max(ntiles, 1);
   if (pps_fixed > 0) {
     const int pps = std::min(pps_fixed, kMaxPps);
     return (ntiles + pps - 1) / pps;
   }
   const long long bh = std::max(1LL, (long long)B * H);
-  long long ns = std::max(1LL, (kTargetWaves + bh / 2) / bh);                 // fill the chip once
-  ns = std::min<long long>(ns, std::max(1, (ntiles + kMinPps - 1) / kMinPps));  // >= kMinPps pages
-  ns = std::max<long long>(ns, (ntiles + kMaxPps - 1) / kMaxPps);              // <= kMaxPps pages
-  return (int)ns;
+  const long long lo = (ntiles + kMaxPps - 1) / kMaxPps;
+  long long ns = lo;
+  for (long long k = 1; k <= 64; ++k) {
+    const long long cand = (k * resident + bh - 1) / bh;
+    if (cand >= lo) { ns = cand; break; }
+  }
+  ns = std::min<long long>(ns, std::max(1, (ntiles + kMinPps - 1) / kMinPps));
+  ns = std::max(ns, lo);
+  return (int)std::min(ns, max_nsplit(B, H, ntiles));
+}
+
+template <int D, int TS>
+long long resident_for(bool direct) {
+  return direct ? resident_waves<D, TS, true>() : resident_waves<D, TS, false>();
+}
+
+long long resident_waves_for(int D, int TS) {
+  auto pick = [&](auto d) -> long long {
+    constexpr int DD = decltype(d)::value;
+    return TS == 16 ? resident_for<DD, 16>(false) : resident_for<DD, 32>(false);
+  };
+  switch (D) {
+    case 32: return pick(std::integral_constant<int, 32>{});
+    case 64: return pick(std::integral_constant<int, 64>{});
+    case 128: return pick(std::integral_constant<int, 128>{});
+    default: return pick(std::integral_constant<int, 256>{});
+  }
 }
 
 }  // namespace
 
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles) {
   const int ntiles = std::max(1, std::min((T + TS - 1) / TS, max_tiles));
-  const int ns = choose_nsplit(B, H, ntiles, 0);
+  const int ns = choose_nsplit(B, H, ntiles, 0, 256LL * 4 * 3);
   return (ntiles + ns - 1) / ns;
 }
 
@@ -364,18 +535,24 @@ extern "C" int pa_decode_pages_per_split(int B, int H, int T, int page_size, int
 extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
                                             int pages_per_split) {
   if (B <= 0 || H <= 0 || D <= 0 || max_tiles <= 0) return 0;
-  const size_t nsplit = (size_t)choose_nsplit(B, H, max_tiles, pages_per_split);
+  const size_t nsplit = pages_per_split > 0
+                            ? (size_t)choose_nsplit(B, H, max_tiles, pages_per_split, 0)
+                            : (size_t)max_nsplit(B, H, max_tiles);
   return (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
 }
 
 int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                             int D, int T, float sm_scale, int pages_per_split, void* workspace,
-                            size_t workspace_bytes, hipStream_t st) {
+                            size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows) {
   LLM_REQUIRE(kv != nullptr, "pa_decode: kv view is NULL");
   LLM_REQUIRE(B >= 0 && H > 0 && D > 0 && T >= 0, "pa_decode: bad B/H/D/T");
   if (B == 0) return LLM_OK;
-  LLM_REQUIRE(q != nullptr && out != nullptr, "pa_decode: q/out NULL");
+  const bool row_out = rows && (rows->q || rows->out16);
+  LLM_REQUIRE(q != nullptr && (out != nullptr || row_out), "pa_decode: q/out NULL");
+  LLM_REQUIRE(!rows || !rows->q || rows->inv_scale, "pa_decode: row quantisation needs inv_scale");
+  LLM_REQUIRE(!row_out || (size_t)H * D * 4 <= 65536, "pa_decode: row outputs need H*D <= 16384");
+  LLM_REQUIRE(!rows || !rows->pack || (H * D) % 64 == 0, "pa_decode: packed row outputs need H*D % 64 == 0");
   LLM_REQUIRE(kv->k_pool && kv->v_pool && kv->page_table, "pa_decode: kv pointers NULL");
   LLM_REQUIRE(kv->kv_dtype == LLM_F16, "pa_decode: only fp16 KV pools are supported");
   LLM_REQUIRE(kv->num_heads == H, "pa_decode: H != kv->num_heads");
@@ -391,8 +568,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // tiles at or past max_tiles have no page-table entry: they are missing (masked)
   const int ntiles_max = std::max(1, std::min((T + TS - 1) / TS, kv->max_tiles));
   const int pps_fixed = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps) : 0;
-  const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed);
+  const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed,
+                                   pps_fixed > 0 ? 0 : resident_waves_for(D, TS));
   const bool direct = nsplit <= 1;
+  LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
 
   PaSplitArgs a{};
   a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
@@ -427,11 +606,27 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     default: e = dispatch_ts<256>(a, TS, direct, st); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
+  if (row_out && !direct) {
+    PaMergeRowArgs mg{a.part_acc, a.part_ml, out, rows->q, rows->inv_scale,
+                      static_cast<_Float16*>(rows->out16), context_lens, B, H, D, T, TS, pps_fixed,
+                      nsplit, kv->max_tiles, rows->pack};
+    const int threads = 64 * std::min(16, H);  // one wave per head (heads > 16 loop)
+    hipLaunchKernelGGL(pa_merge_row_kernel, dim3(B), dim3(threads), (size_t)H * D * sizeof(float),
+                       st, mg);
+    LLM_HIP_RET(hipGetLastError());
+    return LLM_OK;
+  }
   if (!direct) {
     PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, TS, pps_fixed, nsplit,
                    kv->max_tiles};
     hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
     LLM_HIP_RET(hipGetLastError());
+  }
+  if (row_out) {  // single split: out is final; convert it in a row pass
+    if (rows->q)
+      LLM_HIP_RET(launch_quantize_rows(out, B, H * D, rows->q, rows->inv_scale, st, rows->pack));
+    if (rows->out16)
+      LLM_HIP_RET(launch_to_f16(out, (size_t)B * H * D, rows->out16, st, rows->pack ? H * D : 0));
   }
   return LLM_OK;
 }
@@ -453,7 +648,7 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
   LLM_REQUIRE(kv && kv->head_dim == 128 && kv->page_size == 16 && H == kv->num_heads,
               "pa_decode_tune: D=128, page 16 only");
   const int ntiles_max = std::max(1, (T + 15) / 16);
-  pps = std::min(std::max(pps, 1), 64);
+  pps = std::min(std::max(pps, 1), kMaxPps);
   const int nsplit = (ntiles_max + pps - 1) / pps;
   LLM_REQUIRE(nsplit > 1, "pa_decode_tune: needs more than one split");
   const size_t need = (size_t)B * H * nsplit * (128 + 2) * sizeof(float);
@@ -478,6 +673,10 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
     case 3: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2>), grid, block, 0, st, a); break;
     case 4: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 0>), grid, block, 0, st, a); break;
     case 5: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 2>), grid, block, 0, st, a); break;
+    case 6: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 1, 8>), grid, block, 0, st, a); break;
+    case 7: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 1, 4>), grid, block, 0, st, a); break;
+    case 8: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 2, 4>), grid, block, 0, st, a); break;
+    case 9: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 1, 6>), grid, block, 0, st, a); break;
     default: return fail(LLM_ERR_INVALID, "pa_decode_tune: variant");
   }
   LLM_HIP_RET(hipGetLastError());

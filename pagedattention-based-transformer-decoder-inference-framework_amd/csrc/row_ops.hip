@@ -98,6 +98,157 @@ __global__ __launch_bounds__(kRowThreads) void layernorm_quant_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-resident row kernels (cols % 4 == 0, cols <= 1024 * VPT): every
+// thread loads its VPT float4 chunks of the row (chunk i = threadIdx.x + 256 v)
+// with all loads in flight at once, so a row costs ONE memory round trip; the
+// reductions are wave DPP/shuffles + one LDS exchange; int8 results leave as
+// one packed dword per float4.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float block_sum_fast(float v, float* sh) {
+  v = wave_sum(v);
+  __syncthreads();  // sh reuse across consecutive reductions
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (sh[0] + sh[1]) + (sh[2] + sh[3]);  // fixed order: deterministic
+}
+
+__device__ __forceinline__ float block_max_fast(float v, float* sh) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+}
+
+__device__ __forceinline__ uint32_t pack4_i8(f32x4 y, float scale) {
+  const uint32_t b0 = (uint8_t)quant1(y[0], scale), b1 = (uint8_t)quant1(y[1], scale);
+  const uint32_t b2 = (uint8_t)quant1(y[2], scale), b3 = (uint8_t)quant1(y[3], scale);
+  return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+// pack = 1: q / out16 are written in packed-A order (a_frag_off_*), else row-major.
+template <int VPT>
+__global__ __launch_bounds__(kRowThreads) void quantize_rows_v_kernel(
+    const float* __restrict__ x, int cols, int8_t* __restrict__ q, float* __restrict__ inv_scale,
+    int pack) {
+  __shared__ float sh[4];
+  const int r = blockIdx.x;
+  const int n4 = cols >> 2;
+  const f32x4* xr = reinterpret_cast<const f32x4*>(x + (size_t)r * cols);
+  f32x4 v[VPT];
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kRowThreads;
+    v[i] = c < n4 ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(v[i][0]), fabsf(v[i][1])), fmaxf(fabsf(v[i][2]), fabsf(v[i][3]))));
+  am = block_max_fast(am, sh);
+  const float scale = 127.f / (am + 1e-6f);
+  uint32_t* qr = reinterpret_cast<uint32_t*>(q + (size_t)r * cols);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kRowThreads;
+    if (c < n4) {
+      if (pack)
+        *reinterpret_cast<uint32_t*>(q + a_frag_off_i8(r, 4 * c, cols >> 6)) = pack4_i8(v[i], scale);
+      else
+        qr[c] = pack4_i8(v[i], scale);
+    }
+  }
+  if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
+}
+
+template <int VPT>
+__global__ __launch_bounds__(kRowThreads) void layernorm_quant_v_kernel(
+    const float* __restrict__ x, int cols, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
+    float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack) {
+  __shared__ float sh[4];
+  const int r = blockIdx.x;
+  const int n4 = cols >> 2;
+  const f32x4* xr = reinterpret_cast<const f32x4*>(x + (size_t)r * cols);
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma);
+  const f32x4* b4 = reinterpret_cast<const f32x4*>(beta);
+  f32x4 v[VPT], gv[VPT], bv[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kRowThreads;
+    const bool ok = c < n4;
+    v[i] = ok ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    gv[i] = ok ? g4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    bv[i] = ok ? b4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  const float mean = block_sum_fast(s, sh) / (float)cols;
+  float vs = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kRowThreads;
+    if (c < n4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[i][e] - mean;
+        vs = fmaf(d, d, vs);
+      }
+    }
+  }
+  const float var = block_sum_fast(vs, sh) / (float)cols;
+  const float inv_std = (float)(1.0 / (double)sqrtf(var + eps));
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float y = __fmul_rn(__fmul_rn(v[i][e] - mean, inv_std), gv[i][e]);
+      v[i][e] = __fadd_rn(y, bv[i][e]);
+      am = fmaxf(am, fabsf(v[i][e]));
+    }
+    const int c = threadIdx.x + i * kRowThreads;
+    if (c < n4) {
+      if (out) reinterpret_cast<f32x4*>(out + (size_t)r * cols)[c] = v[i];
+      if (out16) {
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        const f16x4 h{(_Float16)v[i][0], (_Float16)v[i][1], (_Float16)v[i][2], (_Float16)v[i][3]};
+        if (pack)
+          *reinterpret_cast<f16x4*>(out16 + a_frag_off_f16(r, 4 * c, cols >> 5)) = h;
+        else
+          reinterpret_cast<f16x4*>(out16 + (size_t)r * cols)[c] = h;
+      }
+    }
+  }
+  if (q) {
+    am = block_max_fast(am, sh);  // padding lanes hold beta=0 -> 0, harmless for |max|
+    const float scale = 127.f / (am + 1e-6f);
+    uint32_t* qr = reinterpret_cast<uint32_t*>(q + (size_t)r * cols);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kRowThreads;
+      if (c < n4) {
+        if (pack)
+          *reinterpret_cast<uint32_t*>(q + a_frag_off_i8(r, 4 * c, cols >> 6)) = pack4_i8(v[i], scale);
+        else
+          qr[c] = pack4_i8(v[i], scale);
+      }
+    }
+    if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
+  }
+}
+
+// VPT (float4 chunks per thread) for a row of `cols`; 0 = use the scalar kernel.
+static int row_vpt(int cols) {
+  if (cols % 4 != 0) return 0;
+  const int n4 = cols / 4;
+  for (int v : {1, 2, 4, 8, 16})
+    if (n4 <= v * kRowThreads) return v;
+  return 0;
+}
+
 // Argmax per row, first maximum wins (std::max_element).
 __global__ __launch_bounds__(kRowThreads) void argmax_kernel(const float* __restrict__ logits,
                                                              int V, int32_t* __restrict__ out,
@@ -170,10 +321,18 @@ __global__ __launch_bounds__(kRowThreads) void kv_append_kernel(
   }
 }
 
-__global__ void to_f16_kernel(const float* __restrict__ x, size_t n, _Float16* __restrict__ y) {
+// pack_cols > 0: y is packed-A fp16 of rows of pack_cols (x row-major [n / pack_cols][pack_cols]).
+__global__ void to_f16_kernel(const float* __restrict__ x, size_t n, _Float16* __restrict__ y,
+                              int pack_cols) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x)
-    y[i] = (_Float16)x[i];
+       i += (size_t)gridDim.x * blockDim.x) {
+    if (pack_cols > 0) {
+      const int m = (int)(i / pack_cols), k = (int)(i % pack_cols);
+      y[a_frag_off_f16(m, k, pack_cols >> 5)] = (_Float16)x[i];
+    } else {
+      y[i] = (_Float16)x[i];
+    }
+  }
 }
 
 // After a step: every row's next position / context length moves by one.
@@ -213,33 +372,61 @@ __global__ void fill_random_f16_kernel(_Float16* __restrict__ p, size_t n, uint6
 // host launchers (internal)
 // ---------------------------------------------------------------------------
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv,
-                                hipStream_t st) {
-  hipLaunchKernelGGL(quantize_rows_kernel, dim3(rows), dim3(kRowThreads), 0, st, x, cols, q, inv);
+                                hipStream_t st, int pack) {
+  const dim3 g(rows), b(kRowThreads);
+  const int v = row_vpt(cols);
+  if (pack && (v == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
+  switch (v) {
+    case 1: hipLaunchKernelGGL(quantize_rows_v_kernel<1>, g, b, 0, st, x, cols, q, inv, pack); break;
+    case 2: hipLaunchKernelGGL(quantize_rows_v_kernel<2>, g, b, 0, st, x, cols, q, inv, pack); break;
+    case 4: hipLaunchKernelGGL(quantize_rows_v_kernel<4>, g, b, 0, st, x, cols, q, inv, pack); break;
+    case 8: hipLaunchKernelGGL(quantize_rows_v_kernel<8>, g, b, 0, st, x, cols, q, inv, pack); break;
+    case 16: hipLaunchKernelGGL(quantize_rows_v_kernel<16>, g, b, 0, st, x, cols, q, inv, pack); break;
+    default: hipLaunchKernelGGL(quantize_rows_kernel, g, b, 0, st, x, cols, q, inv); break;
+  }
+  return hipGetLastError();
+}
+
+static hipError_t launch_ln(const float* x, int rows, int cols, const float* g, const float* b,
+                            float eps, float* out, int8_t* q, float* inv, _Float16* out16,
+                            hipStream_t st, int pack) {
+  const dim3 gr(rows), bl(kRowThreads);
+  const int v = row_vpt(cols);
+  if (pack && (v == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
+  switch (v) {
+#define LN_CASE(V)                                                                              \
+  case V:                                                                                        \
+    hipLaunchKernelGGL(layernorm_quant_v_kernel<V>, gr, bl, 0, st, x, cols, g, b, eps, out, q,   \
+                       inv, out16, pack);                                                        \
+    break;
+    LN_CASE(1) LN_CASE(2) LN_CASE(4) LN_CASE(8) LN_CASE(16)
+#undef LN_CASE
+    default:
+      hipLaunchKernelGGL(layernorm_quant_kernel, gr, bl, (size_t)cols * sizeof(float), st, x, cols,
+                         g, b, eps, out, q, inv, out16);
+      break;
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
-                                  hipStream_t st) {
-  hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
-                     (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv,
-                     (_Float16*)nullptr);
-  return hipGetLastError();
+                                  hipStream_t st, int pack) {
+  return launch_ln(x, rows, cols, g, b, eps, out, q, inv, nullptr, st, pack);
 }
 
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
-                                const float* b, float eps, void* out16, hipStream_t st) {
-  hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
-                     (size_t)cols * sizeof(float), st, x, cols, g, b, eps, (float*)nullptr,
-                     (int8_t*)nullptr, (float*)nullptr, static_cast<_Float16*>(out16));
-  return hipGetLastError();
+                                const float* b, float eps, void* out16, hipStream_t st, int pack) {
+  return launch_ln(x, rows, cols, g, b, eps, nullptr, nullptr, nullptr,
+                   static_cast<_Float16*>(out16), st, pack);
 }
 
-hipError_t launch_to_f16(const float* x, size_t n, void* y, hipStream_t st) {
+hipError_t launch_to_f16(const float* x, size_t n, void* y, hipStream_t st, int pack_cols) {
   if (n == 0) return hipSuccess;
+  if (pack_cols > 0 && pack_cols % 32 != 0) return hipErrorInvalidValue;
   const size_t blocks = std::min<size_t>((n + 255) / 256, 65536);
   hipLaunchKernelGGL(to_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n,
-                     static_cast<_Float16*>(y));
+                     static_cast<_Float16*>(y), pack_cols);
   return hipGetLastError();
 }
 
@@ -295,7 +482,7 @@ extern "C" int quantize_rows(const float* x, int rows, int cols, int8_t* q, floa
   LLM_REQUIRE(rows >= 0 && cols > 0, "quantize_rows: bad shape");
   if (rows == 0) return LLM_OK;
   LLM_REQUIRE(x && q && inv_scale, "quantize_rows: NULL pointer");
-  LLM_HIP_RET(launch_quantize_rows(x, rows, cols, q, inv_scale, as_stream(stream)));
+  LLM_HIP_RET(launch_quantize_rows(x, rows, cols, q, inv_scale, as_stream(stream), 0));
   return LLM_OK;
 }
 
@@ -309,7 +496,7 @@ extern "C" int layernorm_quant(const float* x, int rows, int cols, const float* 
   LLM_REQUIRE(out || q, "layernorm_quant: no output requested");
   LLM_REQUIRE(cols <= 16384, "layernorm_quant: cols > 16384 (LDS row buffer)");
   LLM_HIP_RET(launch_layernorm_quant(x, rows, cols, gamma, beta, eps, out, q, inv_scale,
-                                     as_stream(stream)));
+                                     as_stream(stream), 0));
   return LLM_OK;
 }
 

@@ -33,7 +33,11 @@ def test_abi_version_and_pure_host_helpers():
     # host-only sizing helpers (no device calls)
     assert lib.gemm_packed_bytes(llm_capi.LLM_I8, 2048, 6144) == 6144 // 16 * 2048 // 64 * 1024
     assert lib.gemm_packed_bytes(llm_capi.LLM_F16, 768, 2304) == 2304 // 16 * 768 // 32 * 1024
-    assert lib.pa_decode_pages_per_split(64, 16, 8192, 16, 513) == 64
+    # C3: 64x16 rows x 513 tiles -> 6 splits of <= 86 pages (two full rounds of
+    # the host-side 3072 resident-wave estimate; <= 128 pages per split)
+    assert lib.pa_decode_pages_per_split(64, 16, 8192, 16, 513) == 86
+    # dynamic splits: bounded by ceil(513/128) + ceil(8192/1024) + 1 = 14 splits
+    assert lib.pa_decode_workspace_bytes(64, 16, 128, 513, 0) == 64 * 16 * 14 * 130 * 4
     assert lib.pa_decode_pages_per_split(16, 12, 2048, 16, 128) == 8
     assert lib.pa_decode_workspace_bytes(2, 2, 64, 16, 8) == 2 * 2 * 2 * (64 + 2) * 4
     assert lib.pa_decode_pages_per_split(-1, 1, 1, 16, 1) == -1

@@ -52,6 +52,39 @@ def test_i8_gemm_no_scales(gpu, oracle):
     np.testing.assert_array_equal(C.cpu().numpy(), ref.astype(np.float32))
 
 
+@pytest.mark.parametrize("M,K,N,nt,waves", [
+    (64, 2048, 6144, 2, 8), (64, 8192, 2048, 1, 8), (64, 2048, 2048, 1, 16), (37, 512, 96, 2, 8),
+    (16, 256, 64, 1, 8), (100, 1024, 512, 2, 16),
+])
+def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
+    """The decoder's GEMM form: A in packed-A (MFMA fragment) order, forced
+    column-tile count / waves per workgroup (exported tuning entry
+    i8_gemm_tune): bit-exact against the oracle like the row-major C ABI."""
+    import ctypes
+    import torch
+    import llm_capi
+    lib = llm_capi.load()
+    lib.i8_gemm_tune.restype = ctypes.c_int
+    lib.i8_gemm_tune.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                      ctypes.c_void_p] + [ctypes.c_int] * 3 + \
+        [ctypes.c_void_p] * 3
+    rng = np.random.default_rng(M + K + N + nt)
+    A = rng.integers(-128, 128, (M, K), dtype=np.int8)
+    W = rng.integers(-128, 128, (K, N), dtype=np.int8)
+    sa = rng.uniform(1e-3, 1e-2, M).astype(np.float32)
+    sw = rng.uniform(1e-3, 1e-2, N).astype(np.float32)
+    Wp = llm_capi.pack_weights(_dev(W), llm_capi.LLM_I8)
+    Ap = llm_capi.pack_weights(_dev(np.ascontiguousarray(A.T)), llm_capi.LLM_I8)  # A-fragment order
+    _, ref_C = oracle.i8_gemm(A, W, sa, sw, None, 0)
+    dsa, dsw, dA = _dev(sa), _dev(sw), _dev(A)
+    for packed, a_t in ((1, Ap), (0, dA)):
+        C = torch.full((M, N), float("nan"), device="cuda")
+        llm_capi.check(lib.i8_gemm_tune(nt, waves, packed, a_t.data_ptr(), K, Wp.data_ptr(),
+                                        C.data_ptr(), M, N, K, dsa.data_ptr(), dsw.data_ptr(),
+                                        None))
+        np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
+
+
 @pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (64, 2048, 512), (3, 96, 48), (80, 256, 64)])
 def test_f16_gemm(gpu, M, K, N):
     import llm_capi
