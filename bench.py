@@ -178,13 +178,15 @@ def cpu_baseline(cfg, budget_s=20.0):
 
 
 def load_traffic(cfg_name):
-    """HBM traffic of the attention launch from the committed rocprofv3 --pmc
-    summary (profiles/), if one exists for this config."""
+    """Measured HBM bytes / algorithmic bytes of the attention launch, from the
+    committed rocprofv3 --pmc summary (profiles/pmc_attention_<cfg>.json:
+    (2*FETCH_SIZE + WRITE_SIZE) KiB per launch, gfx950-corrected, over
+    scripts/prof_attention.py at this config), or None."""
     p = ROOT / "profiles" / f"pmc_attention_{cfg_name}.json"
     if not p.exists():
         return None
     try:
-        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+        return float(json.loads(p.read_text())["traffic_over_algorithmic"])
     except Exception:
         return None
 
@@ -276,9 +278,13 @@ def main():
     t_attn = time_attention(dec, cfg, B, T_now, max_seq)
     attn_b = attention_launch_bytes(cfg, T_now, B)
     achieved = attn_b / t_attn / 1e9
+    ratio = load_traffic(args.config)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": load_traffic(args.config),
+            # PMC-measured HBM bytes per launch (ratio from profiles/pmc_attention_<cfg>.json
+            # applied to this launch's algorithmic bytes)
+            "traffic": int(ratio * attn_b) if ratio else None,
+            "traffic_over_algorithmic": ratio,
             "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}> + pa_merge_kernel",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
     step_b = step_bytes(cfg, T_mean, B)

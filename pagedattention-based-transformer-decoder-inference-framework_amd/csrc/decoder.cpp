@@ -178,9 +178,10 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
                                 pa_decode_workspace_bytes(b, d->H, d->D, d->max_tiles, 0));
   RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
   d->qa_ld = std::max(hid, inter);
-  // micro-batch overlap: LLM_MICROBATCHES=1|2 (default 2 for batches >= 2),
+  // micro-batch overlap: LLM_MICROBATCHES=1|2 (default 1: measured slower at C3,
+  // 3596 vs 3623 tok/s — the glue kernels slow down beside a saturating scan),
   // LLM_MB_PINGPONG=0|1, LLM_GRAPH=0|1 (eager launches, for profiling)
-  d->microbatches = env_int("LLM_MICROBATCHES", 2);
+  d->microbatches = env_int("LLM_MICROBATCHES", 1);
   d->pingpong = env_int("LLM_MB_PINGPONG", 1) != 0;
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
   if (d->microbatches >= 2 && B >= 2) {

@@ -41,16 +41,24 @@ pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).resha
 out = torch.empty((B, H, D), device="cuda")
 lib = llm_capi.load()
 view = llm_capi.kv_view(kp, vp, pt)
-pps = lib.pa_decode_pages_per_split(B, H, T, ts, nt)
-ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, nt, pps)
+pps = 0  # production choice: balanced device-side splits
+ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, nt, 0)
 ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device="cuda")
 st = llm_capi.stream_ptr()
+
+
+def launch():
+    llm_capi.check(lib.pa_decode(ctypes.byref(view), llm_capi.ptr(q), llm_capi.ptr(out), None,
+                                 None, B, H, D, T, 1.0, pps, llm_capi.ptr(ws), ws_bytes, st))
+
+
+for _ in range(3):  # warm-up (first-touch / TLB)
+    launch()
 torch.cuda.synchronize()
 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 s.record()
 for _ in range(args.iters):
-    llm_capi.check(lib.pa_decode(ctypes.byref(view), llm_capi.ptr(q), llm_capi.ptr(out), None,
-                                 None, B, H, D, T, 1.0, pps, llm_capi.ptr(ws), ws_bytes, st))
+    launch()
 e.record()
 torch.cuda.synchronize()
 t = s.elapsed_time(e) / args.iters * 1e-3
