@@ -46,6 +46,14 @@ CONFIGS = {
     "c3": dict(cls="INT8Decoder", L=24, H=16, D=128, V=50257, B=64, T=8192, ts=16,
                workload="C3: INT8 decoder (MFMA i8 matmuls + fp16 paged attention), "
                         "24-layer/16-head/d=128, 64 seqs/GPU, KV context 8192, page 16"),
+    # BASELINE.json configs[3]: beam=4 decode over forked prefixes (C3 model dims,
+    # SURVEY §8 C4 build decision): 8 sequences x 4 beams; each sequence's first
+    # 3840 tokens live in shared (forked) pages, each beam holds 256 private tokens
+    "c4": dict(cls="INT8Decoder", L=24, H=16, D=128, V=50257, B=32, T=4096, ts=16,
+               seqs=8, beams=4, shared=3840,
+               workload="C4: beam=4 INT8 decode, 8 seqs x 4 beams (24-layer/16-head/d=128), "
+                        "KV context 4096 = 3840 shared (page-table fork) + 256 per beam, "
+                        "beam-aware attention schedule"),
     # BASELINE.json configs[1]
     "c2": dict(cls="CUDADecoder", L=12, H=12, D=64, V=50257, B=16, T=2048, ts=16,
                workload="C2: fp16 paged decode, 12-layer/12-head/d=64, 16 seqs/GPU, "
@@ -85,24 +93,34 @@ def make_weights(cfg, seed):
 
 def step_bytes(cfg, T_mean, B):
     """Algorithmic HBM bytes of one decode step: fp16 K+V of every
-    row/head/token, page-table entries, int8 weights + fp32 scales, q/out,
-    tied fp16 LM head.  Re-reads are not counted."""
+    row/head/token (shared beam prefixes once per sequence), page-table
+    entries, int8 weights + fp32 scales, q/out, tied fp16 LM head.  Re-reads
+    are not counted."""
     L, H, D, V, ts = cfg["L"], cfg["H"], cfg["D"], cfg["V"], cfg["ts"]
     hid, inter = H * D, 4 * H * D
     nt = (T_mean + ts - 1) / ts
-    attn = 2 * B * H * T_mean * D * 2 + B * H * nt * 4 + 2 * B * hid * 4
+    kv_tokens = B * T_mean
+    if "beams" in cfg:
+        kv_tokens = cfg["seqs"] * cfg["shared"] + B * (T_mean - cfg["shared"])
+    attn = 2 * kv_tokens * H * D * 2 + B * H * nt * 4 + 2 * B * hid * 4
     wbytes = 1 if cfg["cls"] == "INT8Decoder" else 2
     gemm = hid * (3 * hid + hid + 2 * inter) * wbytes + 4 * (3 * hid + hid + inter + hid)
     return L * (attn + gemm) + V * hid * 2
 
 
-def attention_launch_bytes(cfg, T, B):
+def attention_launch_bytes(cfg, T, B, unique=False):
+    """Algorithmic bytes of one attention launch: fp16 K+V of every (row, head,
+    token) + page-table entries + q/out.  unique=True (beam configs) counts
+    each shared prefix page once per sequence (what HBM must deliver)."""
     H, D, ts = cfg["H"], cfg["D"], cfg["ts"]
     nt = (T + ts - 1) // ts
-    return 2 * B * H * T * D * 2 + B * H * nt * 4 + 2 * B * H * D * 4
+    kv_tokens = B * T
+    if unique and "beams" in cfg:
+        kv_tokens = cfg["seqs"] * cfg["shared"] + B * (T - cfg["shared"])
+    return 2 * kv_tokens * H * D * 2 + B * H * nt * 4 + 2 * B * H * D * 4
 
 
-def time_attention(dec, cfg, B, T, max_seq, iters=20):
+def time_attention(dec, cfg, B, T, max_seq, iters=20, row_group=1):
     """Live HIP-event timing of the decoder's paged-attention launch (split +
     merge, the same kernel instantiation and grid as inside the step graph) on
     layer 0's pools, on torch's current stream."""
@@ -120,7 +138,7 @@ def time_attention(dec, cfg, B, T, max_seq, iters=20):
     def run():
         llm_decoder.paged_attention(dec.kv_handle, 0, q.data_ptr(), out.data_ptr(), 0,
                                     ctx.data_ptr(), B, H, D, max_seq, 1.0, 0, 1.0,
-                                    ws.data_ptr(), wsb, st)
+                                    ws.data_ptr(), wsb, st, row_group)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -223,7 +241,11 @@ def main():
     w = make_weights(cfg, args.seed)
     dec.set_weights(w)
     del w
-    dec.begin_synthetic(B, T, args.seed + rank, True)
+    if "beams" in cfg:
+        dec.begin_beams(cfg["seqs"], cfg["beams"], cfg["shared"], T - cfg["shared"],
+                        args.seed + rank, True)
+    else:
+        dec.begin_synthetic(B, T, args.seed + rank, True)
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s")
 
     stream = torch.cuda.current_stream()
@@ -275,8 +297,8 @@ def main():
 
     # roofline of the dominant kernel (paged attention), timed live
     T_now = dec.context_len(0)
-    t_attn = time_attention(dec, cfg, B, T_now, max_seq)
-    attn_b = attention_launch_bytes(cfg, T_now, B)
+    t_attn = time_attention(dec, cfg, B, T_now, max_seq, row_group=cfg.get("beams", 1))
+    attn_b = attention_launch_bytes(cfg, T_now, B, unique=True)
     achieved = attn_b / t_attn / 1e9
     ratio = load_traffic(args.config)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
@@ -287,6 +309,11 @@ def main():
             "traffic_over_algorithmic": ratio,
             "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}> + pa_merge_kernel",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
+    if "beams" in cfg:  # logical bytes: every beam reads its whole context
+        logical = attention_launch_bytes(cfg, T_now, B)
+        roof["bytes_note"] = "achieved counts shared prefix pages once per sequence"
+        roof["logical_bytes_per_launch"] = logical
+        roof["logical_GBps"] = round(logical / t_attn / 1e9, 1)
     step_b = step_bytes(cfg, T_mean, B)
 
     cpu = None

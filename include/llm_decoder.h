@@ -86,6 +86,18 @@ int pa_decode(const pa_kv_view* kv, const float* q, float* out, const int32_t* b
               const int32_t* context_lens, int B, int H, int D, int T, float sm_scale,
               int pages_per_split, void* workspace, size_t workspace_bytes, void* stream);
 
+/* pa_decode with beam-aware scheduling (the beam routing of
+ * paged_flash_attention_kernel_fused.cu:22 plus "beam-aware KV tile prefetch",
+ * README.md:64): rows are taken in groups of row_group (1..4, e.g. the beams of
+ * one sequence, rows g*row_group .. g*row_group+row_group-1); the group's rows
+ * for one (head, split) run as adjacent waves of one workgroup, so KV pages
+ * they share through kv_cache_fork are read from HBM once and re-served from
+ * L2.  Results are identical to pa_decode. */
+int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
+                      const int32_t* context_lens, int B, int H, int D, int T, float sm_scale,
+                      int pages_per_split, int row_group, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* INT8 / FP16 weight GEMMs (MFMA)                                          */
 /* ------------------------------------------------------------------------ */
@@ -239,6 +251,14 @@ int llm_decoder_generate(llm_decoder* d, const int32_t* prompts, const int32_t* 
  * random fp16 K/V on device. */
 int llm_decoder_begin_synthetic(llm_decoder* d, int batch, int context_len, uint64_t seed,
                                 int shuffle);
+/* Start num_seqs * beam_width rows (row = seq * beam_width + beam) for beam
+ * decode: each sequence's first shared_len tokens live in beam 0's pages and
+ * are shared by the other beams through kv_cache_fork (refcounted, copy-on-
+ * write on append); every beam then holds beam_len private tokens.  Pages hold
+ * seeded random fp16 K/V.  Attention runs beam-aware (pa_decode_grouped with
+ * row_group = beam_width, 1..4). */
+int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_width, int shared_len,
+                            int beam_len, uint64_t seed, int shuffle);
 /* One decode step for all active rows: tokens (host [batch], or NULL to feed
  * back the previous argmax) at each row's next position; writes fp32 logits
  * to logits_dev ([batch][V] device, may be NULL) and copies next ids to

@@ -172,6 +172,13 @@ class Decoder {
     check(llm_decoder_begin_synthetic(d_, batch, context_len, seed, shuffle ? 1 : 0));
   }
 
+  void begin_beams(int num_seqs, int beam_width, int shared_len, int beam_len, uint64_t seed,
+                   bool shuffle) {
+    py::gil_scoped_release nogil;
+    check(llm_decoder_begin_beams(d_, num_seqs, beam_width, shared_len, beam_len, seed,
+                                  shuffle ? 1 : 0));
+  }
+
   py::object step(py::object tokens, uintptr_t logits_ptr, uintptr_t stream, bool want_next) {
     std::vector<int32_t> tok;
     const int32_t* tp = nullptr;
@@ -341,6 +348,9 @@ PYBIND11_MODULE(llm_decoder, m) {
              py::arg("max_gen_len"), py::arg("temperature") = 1.0f)
         .def("begin_synthetic", &Decoder::begin_synthetic, py::arg("batch"),
              py::arg("context_len"), py::arg("seed") = 0, py::arg("shuffle") = true)
+        .def("begin_beams", &Decoder::begin_beams, py::arg("num_seqs"), py::arg("beam_width"),
+             py::arg("shared_len"), py::arg("beam_len"), py::arg("seed") = 0,
+             py::arg("shuffle") = true)
         .def("step", &Decoder::step, py::arg("tokens") = py::none(), py::arg("logits_ptr") = 0,
              py::arg("stream") = 0, py::arg("want_next") = true)
         .def("sync", &Decoder::sync)
@@ -399,7 +409,8 @@ PYBIND11_MODULE(llm_decoder, m) {
   m.def("paged_attention",
         [](uintptr_t kv_handle, int layer, uintptr_t q, uintptr_t out, uintptr_t beam_ids,
            uintptr_t context_lens, int B, int H, int D, int T, float temperature, int top_k,
-           float top_p, uintptr_t workspace, size_t workspace_bytes, uintptr_t stream) {
+           float top_p, uintptr_t workspace, size_t workspace_bytes, uintptr_t stream,
+           int row_group) {
           // AttentionCUDA::forward (attention/attention_cuda.cu:41-95) over a KVTileCache.
           if (top_k > 0 || top_p < 1.0f)
             throw std::runtime_error("paged_attention: top-k / top-p attention filters are not "
@@ -408,17 +419,18 @@ PYBIND11_MODULE(llm_decoder, m) {
           check(kv_cache_view(reinterpret_cast<kv_cache*>(kv_handle), layer, &v));
           const float sm = 1.0f / (temperature * temperature);
           py::gil_scoped_release nogil;
-          check(pa_decode(&v, reinterpret_cast<const float*>(q), reinterpret_cast<float*>(out),
-                          reinterpret_cast<const int32_t*>(beam_ids),
-                          reinterpret_cast<const int32_t*>(context_lens), B, H, D, T, sm, 0,
-                          reinterpret_cast<void*>(workspace), workspace_bytes,
-                          reinterpret_cast<void*>(stream)));
+          check(pa_decode_grouped(&v, reinterpret_cast<const float*>(q),
+                                  reinterpret_cast<float*>(out),
+                                  reinterpret_cast<const int32_t*>(beam_ids),
+                                  reinterpret_cast<const int32_t*>(context_lens), B, H, D, T, sm,
+                                  0, row_group, reinterpret_cast<void*>(workspace),
+                                  workspace_bytes, reinterpret_cast<void*>(stream)));
         },
         py::arg("kv_handle"), py::arg("layer"), py::arg("q"), py::arg("out"),
         py::arg("beam_ids") = 0, py::arg("context_lens") = 0, py::arg("B") = 1,
         py::arg("H") = 1, py::arg("D") = 64, py::arg("T") = 1, py::arg("temperature") = 1.0f,
         py::arg("top_k") = 0, py::arg("top_p") = 1.0f, py::arg("workspace") = 0,
-        py::arg("workspace_bytes") = 0, py::arg("stream") = 0);
+        py::arg("workspace_bytes") = 0, py::arg("stream") = 0, py::arg("row_group") = 1);
   m.def("workspace_bytes", &pa_decode_workspace_bytes, py::arg("B"), py::arg("H"), py::arg("D"),
         py::arg("max_tiles"), py::arg("pages_per_split") = 0);
 }

@@ -109,6 +109,7 @@ struct llm_decoder {
 
   // micro-batch overlap (see enqueue_step)
   int microbatches = 1;
+  int row_group = 1;  // beam width of llm_decoder_begin_beams (beam-aware attention)
   bool pingpong = true;
   bool use_graph = true;
   hipStream_t stream2 = nullptr;
@@ -355,7 +356,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const MicroBatch& mb) {
   }
   return pa_decode_internal(&view, qkv.p + (size_t)r0 * hid, hid, o.p + (size_t)r0 * hid, nullptr,
                             ctx.p + r0, B, H, D, cfg.max_seq_len, cfg.attn_scale, pps, mb.attn_ws,
-                            attn_ws_bytes, st, &ro);
+                            attn_ws_bytes, st, &ro, r0 % row_group == 0 ? row_group : 1);
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const MicroBatch& mb) {
@@ -523,6 +524,7 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   LLM_REQUIRE(batch > 0 && batch <= d->maxB, "decoder: batch must be in [1, max_batch]");
   RET_IF(kv_cache_clear(d->kv));
   d->batch = batch;
+  d->row_group = 1;
   d->h_pos.assign(d->maxB, 0);
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
   std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
@@ -556,6 +558,44 @@ extern "C" int llm_decoder_begin_synthetic(llm_decoder* d, int batch, int contex
   LLM_HIP_RET(launch_fill_random_f16(k->k_pool, n, seed * 2 + 1, 0.05f, d->stream));
   LLM_HIP_RET(launch_fill_random_f16(k->v_pool, n, seed * 2 + 2, 1.0f, d->stream));
   LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_width,
+                                       int shared_len, int beam_len, uint64_t seed, int shuffle) {
+  LLM_REQUIRE(d, "llm_decoder_begin_beams: NULL");
+  LLM_REQUIRE(num_seqs > 0 && beam_width >= 1 && beam_width <= 4 && shared_len >= 0 &&
+                  beam_len >= 0,
+              "llm_decoder_begin_beams: bad arguments (beam_width in [1, 4])");
+  std::lock_guard<std::mutex> g(d->mu);
+  const int ctx_len = shared_len + beam_len;
+  LLM_REQUIRE(ctx_len < d->cfg.max_seq_len,
+              "llm_decoder_begin_beams: shared_len + beam_len must be < max_seq_len");
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  const int batch = num_seqs * beam_width;
+  RET_IF(reset_rows(d, batch, ctx_len));
+  KvCache* k = kv_impl(d->kv);
+  if (shuffle) {
+    std::lock_guard<std::mutex> gk(k->mu);
+    std::mt19937_64 rng(seed ^ 7);
+    for (auto& f : k->free_lists) std::shuffle(f.begin(), f.end(), rng);
+  }
+  // beam 0 of each sequence owns the shared prefix; the other beams fork its
+  // page table (shared pages, refcounted) and then get private pages for their
+  // own beam_len tokens.
+  for (int sq = 0; sq < num_seqs; ++sq) {
+    const int b0 = sq * beam_width;
+    RET_IF(kv_cache_reserve(d->kv, b0, shared_len));
+    for (int w = 1; w < beam_width; ++w) RET_IF(kv_cache_fork(d->kv, b0, b0 + w));
+    for (int w = 0; w < beam_width; ++w) RET_IF(kv_cache_reserve(d->kv, b0 + w, ctx_len));
+  }
+  RET_IF(kv_cache_sync(d->kv, d->stream));
+  const size_t n = (size_t)k->num_pages * k->page_elems;
+  LLM_HIP_RET(launch_fill_random_f16(k->k_pool, n, seed * 2 + 1, 0.05f, d->stream));
+  LLM_HIP_RET(launch_fill_random_f16(k->v_pool, n, seed * 2 + 2, 1.0f, d->stream));
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  d->row_group = beam_width;
+  d->graph_batch = -1;  // re-capture: the attention launch depends on row_group
   return LLM_OK;
 }
 

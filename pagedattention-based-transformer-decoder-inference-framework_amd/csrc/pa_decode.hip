@@ -60,6 +60,9 @@ struct PaSplitArgs {
   int num_pages, num_beams, max_tiles;
   int pps;     // > 0: fixed pages per split (<= 128); 0: ceil(ntiles_b / nsplit)
   int nsplit;  // splits per (b, h) (grid)
+  int group;   // rows per wave group (beam width): the group's rows for one (head, split)
+               // run as adjacent waves of one workgroup, so pages the rows share (a
+               // forked prefix) are fetched from HBM once and re-served from L2
   float qscale;
 };
 
@@ -100,11 +103,16 @@ void pa_split_kernel(PaSplitArgs a) {
 
   const int lane = lane_id();
   const int wid = blockIdx.x * 4 + wave_id_uniform();
-  if (wid >= a.B * a.H * a.nsplit) return;
-  const int s = wid % a.nsplit;
-  const int bh = wid / a.nsplit;
-  const int h = bh % a.H;
-  const int b = bh / a.H;
+  const int G = a.group;
+  const int gi = wid % G;  // row within the group (fastest: adjacent waves)
+  const int rest = wid / G;
+  const int s = rest % a.nsplit;
+  const int gh = rest / a.nsplit;
+  const int h = gh % a.H;
+  const int b = (gh / a.H) * G + gi;
+  if (b >= a.B) return;
+  const int bh = b * a.H + h;
+  const size_t pidx = (size_t)bh * a.nsplit + s;  // partial-state slot
   const int r = a.beam_ids ? a.beam_ids[b] : b;
   int Tb = a.context_lens ? a.context_lens[b] : a.T;
   Tb = min(max(Tb, 0), a.T);
@@ -265,12 +273,12 @@ void pa_split_kernel(PaSplitArgs a) {
       *reinterpret_cast<f32x4*>(o + 4) =
           f32x4{acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv};
     } else {
-      float* o = a.part_acc + (size_t)wid * D + c * 8;
+      float* o = a.part_acc + pidx * D + c * 8;
       *reinterpret_cast<f32x4*>(o) = f32x4{acc[0], acc[1], acc[2], acc[3]};
       *reinterpret_cast<f32x4*>(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
       if (lane == 0) {
-        a.part_ml[(size_t)wid * 2] = m;
-        a.part_ml[(size_t)wid * 2 + 1] = l;
+        a.part_ml[pidx * 2] = m;
+        a.part_ml[pidx * 2 + 1] = l;
       }
     }
   }
@@ -443,7 +451,7 @@ long long resident_waves() {
 
 template <int D, int TS>
 hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st) {
-  const int waves = a.B * a.H * a.nsplit;
+  const int waves = ((a.B + a.group - 1) / a.group) * a.group * a.H * a.nsplit;
   const dim3 grid((waves + 3) / 4), block(256);
   if (direct)
     hipLaunchKernelGGL((pa_split_kernel<D, TS, true>), grid, block, 0, st, a);
@@ -544,7 +552,8 @@ extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
 int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                             int D, int T, float sm_scale, int pages_per_split, void* workspace,
-                            size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows) {
+                            size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows,
+                            int row_group) {
   LLM_REQUIRE(kv != nullptr, "pa_decode: kv view is NULL");
   LLM_REQUIRE(B >= 0 && H > 0 && D > 0 && T >= 0, "pa_decode: bad B/H/D/T");
   if (B == 0) return LLM_OK;
@@ -590,6 +599,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   a.max_tiles = kv->max_tiles;
   a.pps = pps_fixed;
   a.nsplit = nsplit;
+  a.group = std::max(1, std::min(row_group, 4));
   a.qscale = sm_scale * kLog2e;
   if (!direct) {
     const size_t need = (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
@@ -631,6 +641,17 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   return LLM_OK;
 }
 
+extern "C" int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* out,
+                                 const int32_t* beam_ids, const int32_t* context_lens, int B,
+                                 int H, int D, int T, float sm_scale, int pages_per_split,
+                                 int row_group, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  LLM_REQUIRE(row_group >= 1 && row_group <= 4, "pa_decode_grouped: row_group must be in [1, 4]");
+  return pa_decode_internal(kv, q, H * D, out, beam_ids, context_lens, B, H, D, T, sm_scale,
+                            pages_per_split, workspace, workspace_bytes, as_stream(stream),
+                            nullptr, row_group);
+}
+
 extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
                          const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                          int D, int T, float sm_scale, int pages_per_split, void* workspace,
@@ -661,12 +682,12 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
   a.context_lens = context_lens;
   a.B = B; a.H = H; a.T = T;
   a.num_pages = kv->num_pages; a.num_beams = kv->num_beams; a.max_tiles = kv->max_tiles;
-  a.pps = pps; a.nsplit = nsplit; a.qscale = kLog2e;
+  a.pps = pps; a.nsplit = nsplit; a.group = 1; a.qscale = kLog2e;
   a.part_acc = static_cast<float*>(workspace);
   a.part_ml = a.part_acc + (size_t)B * H * nsplit * 128;
   hipStream_t st = as_stream(stream);
   const dim3 grid((B * H * nsplit + 3) / 4), block(256);
-  switch (variant) {
+  switch (variant) {  // NOLINT
     case 0: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 0>), grid, block, 0, st, a); break;
     case 1: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2>), grid, block, 0, st, a); break;
     case 2: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 0>), grid, block, 0, st, a); break;

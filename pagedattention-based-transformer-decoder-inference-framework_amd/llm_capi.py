@@ -49,6 +49,9 @@ _SIGS = {
     "pa_decode": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_size_t,
                           c_void_p]),
+    "pa_decode_grouped": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_int,
+                                  c_void_p, c_size_t, c_void_p]),
     "gemm_packed_bytes": (c_size_t, [c_int, c_int, c_int]),
     "gemm_pack_weights": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "i8_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -147,8 +150,9 @@ def kv_view(k_pool, v_pool, page_table, *, num_beams=None) -> PaKvView:
 
 
 def pa_decode(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_lens=None,
-              sm_scale=1.0, pages_per_split=0, out=None, stream=None):
-    """Paged decode attention on torch device tensors; returns out [B][H][D] fp32."""
+              sm_scale=1.0, pages_per_split=0, out=None, stream=None, row_group=1):
+    """Paged decode attention on torch device tensors; returns out [B][H][D] fp32.
+    row_group > 1 uses the beam-aware schedule (pa_decode_grouped)."""
     import torch
     lib = load()
     B, H, D = q.shape
@@ -157,9 +161,14 @@ def pa_decode(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_lens=N
     view = kv_view(k_pool, v_pool, page_table)
     ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, page_table.shape[2], pages_per_split)
     ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=q.device)
-    check(lib.pa_decode(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids), ptr(context_lens),
-                        B, H, D, T, sm_scale, pages_per_split, ptr(ws), ws_bytes,
-                        stream_ptr(stream)))
+    if row_group > 1:
+        check(lib.pa_decode_grouped(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids),
+                                    ptr(context_lens), B, H, D, T, sm_scale, pages_per_split,
+                                    row_group, ptr(ws), ws_bytes, stream_ptr(stream)))
+    else:
+        check(lib.pa_decode(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids),
+                            ptr(context_lens), B, H, D, T, sm_scale, pages_per_split, ptr(ws),
+                            ws_bytes, stream_ptr(stream)))
     return out
 
 

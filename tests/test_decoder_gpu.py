@@ -314,3 +314,29 @@ def test_int8_flip_rate(gpu, oracle):
     qr, _ = oracle.quantize_rows(oracle.layer_norm(x, g, b))
     d = np.abs(q.cpu().numpy().astype(np.int32) - qr.astype(np.int32))
     assert d.max() <= 1 and (d > 0).mean() < 1e-4
+
+
+def test_beam_decode_forked_prefix(gpu, oracle):
+    """llm_decoder_begin_beams: 2 sequences x 4 beams over one forked prefix
+    (beam_len 0, so every beam of a sequence holds the SAME context through
+    shared pages).  Fed the same token, the beams of a sequence must produce
+    bitwise identical logits (beam-aware attention, copy-on-write append into
+    the first private tile), sequences differ, and the page pool holds one
+    prefix copy per sequence plus the beams' private append tiles."""
+    torch = _torch()
+    w = _int8_model(oracle, L=2, H=4, D=64, V=500, S=128, seed=9)
+    dec = _make_gpu_decoder(w, max_batch=8)
+    seqs, W, prefix = 2, 4, 40  # 2.5 tiles shared: the partial 3rd tile is copied on write
+    dec.begin_beams(seqs, W, prefix, 0, 3, True)
+    V = w["cfg"]["V"]
+    logits = torch.empty((seqs * W, V), device="cuda")
+    for step in range(3):
+        dec.step([11, 11, 11, 11, 7, 7, 7, 7] if step == 0 else None, logits_ptr=logits.data_ptr())
+        torch.cuda.synchronize()
+        lg = logits.cpu().numpy()
+        assert np.isfinite(lg).all()
+        for sq in range(seqs):
+            for b in range(1, W):
+                np.testing.assert_array_equal(lg[sq * W + b], lg[sq * W])
+        assert not np.array_equal(lg[0], lg[W])
+    assert dec.context_len(0) == prefix + 3

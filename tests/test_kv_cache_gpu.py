@@ -121,6 +121,13 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
     ref = oracle.paged_attention(q, kpool.float().cpu().numpy(), vpool.float().cpu().numpy(),
                                  table.cpu().numpy(), T=T, beam_ids=beam_ids)
     assert rel_err(out, ref) < 1e-3
+    # beam-aware schedule (rows in groups of 2 and 4, B not a multiple of the
+    # group): bitwise identical to the plain schedule
+    for g in (2, 4):
+        outg = llm_capi.pa_decode(torch.from_numpy(q).cuda(), kpool, vpool, table, T=T,
+                                  beam_ids=torch.from_numpy(beam_ids).cuda(),
+                                  row_group=g).cpu().numpy()
+        np.testing.assert_array_equal(outg, out)
     # save / load round trip
     path = str(tmp_path / "kv.bin")
     kv.save_to_file(path)
@@ -137,3 +144,41 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
     # bitwise (rows past the written tokens are never-written bits, possibly NaN)
     assert torch.equal(kpool2[used].view(torch.int16), kpool[used].view(torch.int16))
     assert kv2.free_pages() == kv.free_pages()
+
+
+def test_grouped_attention_shared_prefix_random(gpu, oracle):
+    """Beam-aware pa_decode_grouped on 3 sequences x 4 beams sharing a prefix
+    of pages (the page table rows of a sequence's beams alias the same page
+    ids), ragged per-row contexts: equal to the oracle and to pa_decode."""
+    import torch
+    import llm_capi
+    rng = np.random.default_rng(8)
+    seqs, W, H, D, ts, T = 3, 4, 4, 64, 16, 700
+    B = seqs * W
+    nt = (T + ts - 1) // ts
+    shared = 30  # tiles shared by the beams of a sequence
+    num_pages = seqs * H * shared + B * H * (nt - shared) + 3
+    perm = rng.permutation(num_pages).astype(np.int32)
+    pt = np.full((B, H, nt), -1, np.int32)
+    i = 0
+    for sq in range(seqs):
+        blk = perm[i:i + H * shared].reshape(H, shared)
+        i += H * shared
+        for w in range(W):
+            pt[sq * W + w, :, :shared] = blk
+    for b in range(B):
+        pt[b, :, shared:] = perm[i:i + H * (nt - shared)].reshape(H, nt - shared)
+        i += H * (nt - shared)
+    kp = (rng.standard_normal((num_pages, ts, D)) * D ** -0.25).astype(np.float16)
+    vp = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
+    q = (rng.standard_normal((B, H, D)) * D ** -0.25).astype(np.float32)
+    lens = rng.integers(shared * ts, T + 1, size=B).astype(np.int32)
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T,
+                                 context_lens=lens)
+    d = lambda a: torch.from_numpy(a).cuda()
+    plain = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens)).cpu().numpy()
+    assert rel_err(plain, ref) < 1e-3
+    for g in (2, 4):
+        outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                                  row_group=g).cpu().numpy()
+        np.testing.assert_array_equal(outg, plain)
