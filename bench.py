@@ -225,9 +225,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LLM_DIST_BACKEND=gloo: rehearsal of the N-rank path on fewer GPUs (ranks
+    # share devices round-robin, logits gathered through host memory); the
+    # real multi-GPU run is one rank per GPU over RCCL ("nccl").
+    backend = os.environ.get("LLM_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import llm_decoder  # noqa: F401  (fails loudly if the HIP build is missing)
 
     cfg = CONFIGS[args.config]
@@ -251,7 +259,9 @@ def main():
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     logits = [torch.empty((B, cfg["V"]), device="cuda") for _ in range(2)]
-    gather_bufs = ([[torch.empty_like(logits[0]) for _ in range(world)] for _ in range(2)]
+    host_gather = world > 1 and backend != "nccl"
+    gather_bufs = ([[torch.empty_like(logits[0], device="cpu" if host_gather else "cuda")
+                     for _ in range(world)] for _ in range(2)]
                    if world > 1 and rank == 0 else [None, None])
     works = [None, None]
     tokens = np.random.default_rng(args.seed + rank).integers(0, cfg["V"], B).astype(np.int32)
@@ -263,7 +273,9 @@ def main():
         dec.step(list(map(int, tokens)) if first else None,
                  logits_ptr=logits[slot].data_ptr() if world > 1 else 0,
                  stream=sp, want_next=False)
-        if world > 1:
+        if host_gather:
+            dist.gather(logits[slot].cpu(), gather_bufs[slot] if rank == 0 else None, dst=0)
+        elif world > 1:
             works[slot] = dist.gather(logits[slot], gather_bufs[slot] if rank == 0 else None,
                                       dst=0, async_op=True)
 
@@ -288,7 +300,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed], device="cpu" if host_gather else "cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     t_step = elapsed / args.steps
@@ -340,7 +352,8 @@ def main():
             "data": "synthetic (random-init weights, random fp16 KV context, shuffled pages)",
             "config": {"workload": cfg["workload"], "global_batch": B * world,
                        "batch_per_gpu": B, "seq_len": T, "page_size": cfg["ts"],
-                       "parallelism": f"batch-sharded x{world} (RCCL logits gather to rank 0)"},
+                       "parallelism": f"batch-sharded x{world} (RCCL logits gather to rank 0)"
+                       if not host_gather else f"batch-sharded x{world} ({backend} rehearsal)"},
             "hbm_roofline_frac_step": round(step_b / t_step / 1e9 / HBM_PEAK_GBPS, 4),
             "step_bytes": int(step_b),
             "roofline": roof,
