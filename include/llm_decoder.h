@@ -133,6 +133,22 @@ int lm_head(const float* x, const void* E, float* logits, int M, int V, int K, v
 /* Row-wise argmax (first maximum wins, std::max_element, decoder/cuda_decoder.cu:7-14). */
 int argmax_rows(const float* logits, int rows, int V, int32_t* out, void* stream);
 
+/* Device token sampling per row, reference semantics of
+ * top_k_top_p_filter (attention/top_k_top_p_filter.cuh:55-111) and
+ * apply_topk_topp_filter (attention_cpu/softmax_lut.cpp:233-256):
+ *   p = softmax(logits / temperature) (max-subtracted, sum + 1e-6);
+ *   token i is dropped if its probability rank >= top_k (top_k > 0) or if the
+ *   probability mass ranked above it is >= top_p (top_p < 1);
+ *   the kept mass is sampled by inverse CDF in token-index order with
+ *   u = sample_uniform_host(seed, row, counter) in [0, 1).
+ * temperature <= 0 or top_k == 1: greedy argmax (cuda_decoder.cu:7-14).
+ * V <= 65536. */
+int sample_rows(const float* logits, int rows, int V, float temperature, int top_k, float top_p,
+                uint64_t seed, int counter, int32_t* out, void* stream);
+/* The uniform draw sample_rows uses for (seed, row, counter): splitmix64 of
+ * seed ^ (row << 32) ^ counter, top 24 bits / 2^24. */
+float sample_uniform_host(uint64_t seed, int row, int counter);
+
 /* Per-row dynamic int8 quantisation (attention_cpu/int8_quant.cpp:5-13,59-64):
  * scale_r = 127/(absmax_r + 1e-6); q = clamp(round(x*scale_r)); inv_scale[r] = 1/scale_r. */
 int quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv_scale, void* stream);
@@ -244,6 +260,13 @@ int llm_quantize_weights(const char* fp32_dir, const char* int8_dir, int num_lay
 int llm_decoder_generate(llm_decoder* d, const int32_t* prompts, const int32_t* prompt_lens,
                          int prompt_stride, int batch, int max_gen_len, float temperature,
                          int32_t* out);
+
+/* Token choice of every following step: greedy argmax (temperature <= 0 or
+ * top_k == 1; the default, sample_from_logits, decoder/cuda_decoder.cu:7-14)
+ * or device sampling with temperature / top_k / top_p (sample_rows; the draw
+ * counter of a row is its position, so runs are replayable for a seed). */
+int llm_decoder_set_sampling(llm_decoder* d, float temperature, int top_k, float top_p,
+                             uint64_t seed);
 
 /* Low-level stepping (bench / multi-GPU driver). */
 /* Start `batch` rows whose first context_len tokens are synthetic: every page

@@ -289,3 +289,64 @@ def shuffled_page_table(rng, num_beams, H, max_tiles, ntiles, num_pages=None, mi
     for (b, h, t) in missing:
         pt[b, h, t] = -1
     return pt
+
+
+# ---------------------------------------------------------------------------
+# Token sampling: numpy restatement of the filter in
+# top_k_top_p_filter (attention/top_k_top_p_filter.cuh:55-111) and
+# apply_topk_topp_filter (attention_cpu/softmax_lut.cpp:233-256), with the
+# build's defined draw (sample_uniform: splitmix64, 24 bits).
+# ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def sample_uniform(seed: int, row: int, counter: int) -> float:
+    z = (seed ^ ((row & 0xFFFFFFFF) << 32) ^ (counter & 0xFFFFFFFF)) & _M64
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    z ^= z >> 31
+    return float(np.float32(z >> 40) * np.float32(1.0 / 16777216.0))
+
+
+def sample_rows(logits, temperature=1.0, top_k=0, top_p=1.0, seed=0, counter=0):
+    """Returns (tokens int32 [R], margin [R]): margin = relative distance of the
+    draw from the nearest CDF boundary (small margins may legitimately differ
+    from a device run whose float sums are ordered differently)."""
+    logits = np.asarray(logits, np.float32)
+    R, V = logits.shape
+    toks = np.zeros(R, np.int32)
+    margin = np.full(R, np.inf)
+    for r in range(R):
+        row = logits[r]
+        if temperature <= 0 or top_k == 1:
+            toks[r] = int(np.argmax(row))  # first maximum
+            continue
+        x = row / np.float32(temperature)
+        e = np.exp((x - x.max()).astype(np.float32)).astype(np.float32)
+        p = (e * np.float32(1.0 / (np.float64(e.sum(dtype=np.float64)) + 1e-6))).astype(np.float32)
+        keep = np.ones(V, bool)
+        if 0 < top_k < V:
+            kth = np.sort(p)[-top_k]
+            keep &= p >= kth
+        if top_p < 1.0:
+            order = np.argsort(-p, kind="stable")
+            ps = p[order].astype(np.float64)
+            cum_before = np.cumsum(ps) - ps
+            # ties: the mass strictly above p_i (equal probabilities share it)
+            uniq, first = np.unique(-ps, return_index=True)
+            above = dict(zip(uniq, cum_before[first]))
+            cb = np.array([above[-v] for v in ps])
+            kp = np.zeros(V, bool)
+            kp[order] = cb < top_p
+            keep &= kp
+        q = np.where(keep, p, 0).astype(np.float64)
+        Z = q.sum()
+        target = np.float32(sample_uniform(seed, r, counter)) * np.float32(Z)
+        cdf = np.cumsum(q)
+        i = int(np.searchsorted(cdf, target, side="right"))
+        i = min(i, int(np.nonzero(q)[0][-1]))
+        toks[r] = i
+        bnd = np.abs(cdf[q > 0] - target)
+        margin[r] = bnd.min() / max(Z, 1e-30)
+    return toks, margin

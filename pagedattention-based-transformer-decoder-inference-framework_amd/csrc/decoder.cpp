@@ -110,6 +110,12 @@ struct llm_decoder {
   // micro-batch overlap (see enqueue_step)
   int microbatches = 1;
   int row_group = 1;  // beam width of llm_decoder_begin_beams (beam-aware attention)
+  // sampling (llm_decoder_set_sampling); greedy argmax by default, as the
+  // reference's sample_from_logits (decoder/cuda_decoder.cu:7-14)
+  float temperature = 0.f;
+  int top_k = 0;
+  float top_p = 1.f;
+  uint64_t sample_seed = 0;
   bool pingpong = true;
   bool use_graph = true;
   hipStream_t stream2 = nullptr;
@@ -408,7 +414,11 @@ int llm_decoder::step_tail(hipStream_t st, const MicroBatch& mb) {
   const int r0 = mb.r0;
   float* lg = logits.p + (size_t)r0 * V;
   RET_IF(lm_head(x.p + (size_t)r0 * hid, emb.p, lg, mb.n, V, hid, st));
-  LLM_HIP_RET(launch_argmax(lg, mb.n, V, tokens.p + r0, nullptr, 0, st));  // next tokens in place
+  if (temperature > 0.f && top_k != 1)  // draw counter = the row's position
+    LLM_HIP_RET(launch_sample(lg, mb.n, r0, V, temperature, top_k, top_p, sample_seed, pos.p + r0,
+                              tokens.p + r0, st));
+  else
+    LLM_HIP_RET(launch_argmax(lg, mb.n, V, tokens.p + r0, nullptr, 0, st));  // next tokens in place
   LLM_HIP_RET(launch_advance(pos.p + r0, ctx.p + r0, mb.n, st));
   return LLM_OK;
 }
@@ -596,6 +606,21 @@ extern "C" int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_wi
   LLM_HIP_RET(hipStreamSynchronize(d->stream));
   d->row_group = beam_width;
   d->graph_batch = -1;  // re-capture: the attention launch depends on row_group
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_set_sampling(llm_decoder* d, float temperature, int top_k, float top_p,
+                                        uint64_t seed) {
+  LLM_REQUIRE(d, "llm_decoder_set_sampling: NULL");
+  LLM_REQUIRE(top_k >= 0 && top_p > 0.f && top_p <= 1.f && d->V <= 65536,
+              "llm_decoder_set_sampling: top_k >= 0, 0 < top_p <= 1, vocab <= 65536");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  d->temperature = temperature;
+  d->top_k = top_k;
+  d->top_p = top_p;
+  d->sample_seed = seed;
+  d->graph_batch = -1;  // the step graph changes
   return LLM_OK;
 }
 

@@ -29,6 +29,10 @@ hipError_t launch_kv_append(const float* qkv, int rows, int H, int D, const int3
                             int num_pages, void* k_pool, void* v_pool, hipStream_t st);
 hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* val, int n,
                               hipStream_t st);
+// Device sampling (csrc/sample.hip); counter[r] is the per-row draw counter.
+hipError_t launch_sample(const float* logits, int rows, int row0, int V, float temperature,
+                         int top_k, float top_p, uint64_t seed, const int32_t* counter,
+                         int32_t* out, hipStream_t st);
 hipError_t launch_fill_random_f16(void* p, size_t n, uint64_t seed, float scale, hipStream_t st);
 
 }  // namespace llm

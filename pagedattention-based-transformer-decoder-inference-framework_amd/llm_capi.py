@@ -60,6 +60,9 @@ _SIGS = {
                          c_int, c_void_p]),
     "lm_head": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "argmax_rows": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sample_rows": (c_int, [c_void_p, c_int, c_int, c_float, c_int, c_float, ctypes.c_uint64,
+                            c_int, c_void_p, c_void_p]),
+    "sample_uniform_host": (c_float, [ctypes.c_uint64, c_int, c_int]),
     "quantize_rows": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "layernorm_quant": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p,
                                 c_void_p, c_void_p, c_void_p]),
@@ -220,6 +223,17 @@ def argmax_rows(logits, stream=None):
     R, V = logits.shape
     out = torch.empty(R, dtype=torch.int32, device=logits.device)
     check(lib.argmax_rows(ptr(logits), R, V, ptr(out), stream_ptr(stream)))
+    return out
+
+
+def sample_rows(logits, temperature=1.0, top_k=0, top_p=1.0, seed=0, counter=0, stream=None):
+    """Device sampling of one token per row of fp32 logits [R][V] -> int32 [R]."""
+    import torch
+    lib = load()
+    R, V = logits.shape
+    out = torch.empty(R, dtype=torch.int32, device=logits.device)
+    check(lib.sample_rows(ptr(logits), R, V, temperature, top_k, top_p, seed, counter, ptr(out),
+                          stream_ptr(stream)))
     return out
 
 

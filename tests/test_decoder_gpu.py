@@ -340,3 +340,29 @@ def test_beam_decode_forked_prefix(gpu, oracle):
                 np.testing.assert_array_equal(lg[sq * W + b], lg[sq * W])
         assert not np.array_equal(lg[0], lg[W])
     assert dec.context_len(0) == prefix + 3
+
+
+def test_decoder_device_sampling(gpu, oracle):
+    """llm_decoder_set_sampling: the step graph draws with sample_rows at each
+    row's position (draw counter) — the next ids equal the oracle sampler on
+    the step's own logits; temperature 0 restores greedy argmax."""
+    torch = _torch()
+    from oracle.oracle import sample_rows
+    w = _int8_model(oracle, L=2, H=4, D=64, V=700, S=64, seed=4)
+    dec = _make_gpu_decoder(w, max_batch=4)
+    V = w["cfg"]["V"]
+    dec.set_sampling(0.8, 40, 0.9, 77)
+    dec.begin_synthetic(4, 0, 0, False)
+    logits = torch.empty((4, V), device="cuda")
+    toks = [3, 1, 4, 1]
+    for s in range(4):
+        nxt = dec.step(toks, logits_ptr=logits.data_ptr(), want_next=True)
+        torch.cuda.synchronize()
+        ref, margin = sample_rows(logits.cpu().numpy(), 0.8, 40, 0.9, seed=77, counter=s)
+        ok = (np.asarray(nxt) == ref) | (margin < 1e-4)
+        assert ok.all(), (s, nxt, ref, margin)
+        toks = list(map(int, nxt))
+    dec.set_sampling(0.0, 0, 1.0, 0)
+    nxt = dec.step(toks, logits_ptr=logits.data_ptr(), want_next=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(np.asarray(nxt), logits.cpu().numpy().argmax(1))

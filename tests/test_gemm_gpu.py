@@ -152,3 +152,45 @@ def test_layernorm_quant(gpu, oracle):
     dq = np.abs(q.cpu().numpy().astype(np.int32) - qr.astype(np.int32))
     assert dq.max() <= 1 and (dq > 0).mean() < 1e-3
     np.testing.assert_allclose(s.cpu().numpy(), sr, rtol=1e-5)
+
+
+@pytest.mark.parametrize("V", [1000, 50257])
+@pytest.mark.parametrize("T,k,p", [(0.0, 0, 1.0), (1.0, 1, 1.0), (1.0, 0, 1.0), (0.7, 50, 1.0),
+                                   (1.2, 0, 0.9), (1.0, 20, 0.8), (0.5, 0, 0.5)])
+def test_sample_rows_vs_oracle(gpu, oracle, V, T, k, p):
+    """Device sampling (temperature / top-k / top-p) against
+    the oracle's restatement with the same counter-based draw: same token per
+    row, except where the draw lands within 1e-4 of a CDF boundary."""
+    import llm_capi
+    from oracle.oracle import sample_rows, sample_uniform
+    lib = llm_capi.load()
+    assert abs(lib.sample_uniform_host(7, 3, 11) - sample_uniform(7, 3, 11)) == 0.0
+    rng = np.random.default_rng(V + int(T * 10) + k)
+    logits = (rng.standard_normal((6, V)) * 3).astype(np.float32)
+    for counter in (0, 1, 17):
+        got = llm_capi.sample_rows(_dev(logits), T, k, p, seed=5, counter=counter).cpu().numpy()
+        ref, margin = sample_rows(logits, T, k, p, seed=5, counter=counter)
+        ok = (got == ref) | (margin < 1e-4)
+        assert ok.all(), (counter, got, ref, margin)
+        if T > 0 and k > 1:  # the token is within the top-k
+            for r in range(6):
+                assert logits[r, got[r]] >= np.sort(logits[r])[-k]
+
+
+def test_sample_rows_distribution(gpu):
+    """Frequencies of 4000 draws (counters 0..3999) of an 8-token distribution
+    match softmax(logits / T) within 5 sigma; top-k keeps only the top tokens."""
+    import torch
+    import llm_capi
+    logits = np.array([[2.0, 1.0, 0.5, 0.0, -0.5, -1.0, 1.5, 0.2]], np.float32)
+    T = 0.9
+    pr = np.exp(logits[0] / T - (logits[0] / T).max())
+    pr /= pr.sum()
+    d = _dev(logits)
+    n = 4000
+    toks = torch.stack([llm_capi.sample_rows(d, T, 0, 1.0, seed=123, counter=c) for c in range(n)])
+    cnt = np.bincount(toks.cpu().numpy().ravel(), minlength=8)
+    sigma = np.sqrt(n * pr * (1 - pr))
+    assert np.all(np.abs(cnt - n * pr) < 5 * sigma + 1), (cnt, n * pr)
+    tk = torch.stack([llm_capi.sample_rows(d, T, 3, 1.0, seed=9, counter=c) for c in range(300)])
+    assert set(tk.cpu().numpy().ravel().tolist()) <= {0, 6, 1}
