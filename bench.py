@@ -326,6 +326,8 @@ def main():
         roof["bytes_note"] = "achieved counts shared prefix pages once per sequence"
         roof["logical_bytes_per_launch"] = logical
         roof["logical_GBps"] = round(logical / t_attn / 1e9, 1)
+        t_plain = time_attention(dec, cfg, B, T_now, max_seq, row_group=1)
+        roof["ungrouped_launch_us"] = round(t_plain * 1e6, 2)  # same launch, plain schedule
     step_b = step_bytes(cfg, T_mean, B)
 
     cpu = None
