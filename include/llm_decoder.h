@@ -261,6 +261,14 @@ int llm_decoder_generate(llm_decoder* d, const int32_t* prompts, const int32_t* 
                          int prompt_stride, int batch, int max_gen_len, float temperature,
                          int32_t* out);
 
+/* Chunked prefill (the is_prefill pass of AttentionCUDA::forward,
+ * attention/attention_cuda.hpp:21): append the n tokens (host ids) of active
+ * row `row` at its next positions in one layer pass per chunk of <= 512 tokens
+ * (M = chunk weight GEMMs; causal paged attention per token), then set the
+ * row's next token from the last token's logits, so llm_decoder_step(tokens =
+ * NULL) continues decoding.  llm_decoder_generate uses it for every prompt. */
+int llm_decoder_prefill(llm_decoder* d, int row, const int32_t* tokens, int n);
+
 /* Token choice of every following step: greedy argmax (temperature <= 0 or
  * top_k == 1; the default, sample_from_logits, decoder/cuda_decoder.cu:7-14)
  * or device sampling with temperature / top_k / top_p (sample_rows; the draw

@@ -172,6 +172,11 @@ class Decoder {
     check(llm_decoder_begin_synthetic(d_, batch, context_len, seed, shuffle ? 1 : 0));
   }
 
+  void prefill(int row, const std::vector<int32_t>& tokens) {
+    py::gil_scoped_release nogil;
+    check(llm_decoder_prefill(d_, row, tokens.data(), (int)tokens.size()));
+  }
+
   void set_sampling(float temperature, int top_k, float top_p, uint64_t seed) {
     py::gil_scoped_release nogil;
     check(llm_decoder_set_sampling(d_, temperature, top_k, top_p, seed));
@@ -353,6 +358,7 @@ PYBIND11_MODULE(llm_decoder, m) {
              py::arg("max_gen_len"), py::arg("temperature") = 1.0f)
         .def("begin_synthetic", &Decoder::begin_synthetic, py::arg("batch"),
              py::arg("context_len"), py::arg("seed") = 0, py::arg("shuffle") = true)
+        .def("prefill", &Decoder::prefill, py::arg("row"), py::arg("tokens"))
         .def("set_sampling", &Decoder::set_sampling, py::arg("temperature"),
              py::arg("top_k") = 0, py::arg("top_p") = 1.0f, py::arg("seed") = 0)
         .def("begin_beams", &Decoder::begin_beams, py::arg("num_seqs"), py::arg("beam_width"),

@@ -124,13 +124,23 @@ struct llm_decoder {
   DevBuf<uint8_t> attn_ws2;
   int qa_ld = 0;
 
-  int layer_pre(int l, hipStream_t st, const struct MicroBatch& mb);
-  int layer_attn(int l, hipStream_t st, const struct MicroBatch& mb);
-  int layer_post(int l, hipStream_t st, const struct MicroBatch& mb);
-  int step_head(hipStream_t st, const struct MicroBatch& mb);
-  int step_tail(hipStream_t st, const struct MicroBatch& mb);
+  int layer_pre(int l, hipStream_t st, const struct Rows& R);
+  int layer_attn(int l, hipStream_t st, const struct Rows& R);
+  int layer_post(int l, hipStream_t st, const struct Rows& R);
+  struct Rows step_rows(int r0, int n, uint8_t* ws);
+  int step_head(hipStream_t st, int r0, int n);
+  int step_tail(hipStream_t st, int r0, int n);
   int enqueue_step(hipStream_t st);
   int run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host, hipStream_t st);
+
+  // chunked prefill (llm_decoder_prefill): buffers for one chunk of tokens
+  static constexpr int kPrefillChunk = 512;
+  DevBuf<float> px, pq, po, ph1, psa;
+  DevBuf<uint8_t> pact, pws;
+  DevBuf<int32_t> pmeta;  // [4][chunk]: pos, ctx, page-table row, token
+  size_t pws_bytes = 0;
+  int pf_cap = 0;
+  int prefill(int row, const int32_t* toks, int n, hipStream_t st);
 };
 
 static int check_cfg(const llm_decoder_config& c) {
@@ -303,9 +313,24 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
 // Rows [r0, r0 + n) of the batch: every activation / state buffer is
 // row-indexed, so a micro-batch is a set of offset pointers (plus its own
 // attention workspace).
-struct MicroBatch {
-  int r0 = 0, n = 0;
+// The rows one layer pass works on: a decode micro-batch (rows r0.. of the
+// step buffers, one token each) or a prefill chunk (n tokens of one sequence,
+// beam_rows[m] = its page-table row).  Every buffer is row-indexed.
+struct Rows {
+  int n = 0;
+  float* x = nullptr;   // [n][hid] residual-free hidden state
+  float* q = nullptr;   // [n][hid] q of the fused qkv projection
+  float* o = nullptr;   // [n][hid] attention output (fp32)
+  float* h1 = nullptr;  // [n][inter]
+  void* act = nullptr;  // packed-A GEMM input (int8 or fp16), 16-row tiles
+  float* sa = nullptr;  // [n] int8 row scales
+  const int32_t* pos = nullptr;  // [n] position written this pass
+  const int32_t* ctx = nullptr;  // [n] context length attended (pos + 1)
+  const int32_t* beam_rows = nullptr;  // page-table row per row; NULL: table_row0 + m
+  int table_row0 = 0;
+  int row_group = 1;
   uint8_t* attn_ws = nullptr;
+  size_t attn_ws_bytes = 0;
 };
 
 // Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
@@ -314,112 +339,126 @@ struct MicroBatch {
 // every GEMM A load is one coalesced 1 KiB read.  Micro-batches start on
 // 16-row boundaries, so a row offset r0 is the same base offset in both
 // layouts (r0 * K elements).
-int llm_decoder::layer_pre(int l, hipStream_t st, const MicroBatch& mb) {
-  const int r0 = mb.r0, B = mb.n;
+int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   const size_t lh = (size_t)l * hid;
-  float* xr = x.p + (size_t)r0 * hid;
-  float* qr = qkv.p + (size_t)r0 * hid;  // q only: K and V go straight into the pages
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
-  const KvAppendView app{pos.p + r0, view.page_table + (size_t)r0 * H * view.max_tiles,
-                         kv_cache_k_pool(kv), kv_cache_v_pool(kv), view.num_beams - r0,
-                         view.max_tiles, TS, view.num_pages, H, D};
+  KvAppendView app;
+  app.pos = R.pos;
+  app.page_table = view.page_table + (size_t)R.table_row0 * H * view.max_tiles;
+  app.rows = R.beam_rows;
+  app.k_pool = kv_cache_k_pool(kv);
+  app.v_pool = kv_cache_v_pool(kv);
+  app.num_beams = view.num_beams - R.table_row0;
+  app.max_tiles = view.max_tiles;
+  app.page_size = TS;
+  app.num_pages = view.num_pages;
+  app.H = H;
+  app.D = D;
   WeightGemm g;
   g.dtype = wdtype;
   g.a_packed = 1;
+  g.A = R.act;
   g.W_packed = wqkv.p + sz_qkv * l;
-  g.M = B; g.N = 3 * hid; g.K = hid;
-  g.C = qr; g.c_cols = hid; g.c_ld = hid;
+  g.M = R.n; g.N = 3 * hid; g.K = hid;
+  g.C = R.q; g.c_cols = hid; g.c_ld = hid;  // q only: K and V go straight into the pages
   g.kv = &app;
   if (wdtype == LLM_I8) {
-    int8_t* qar = qa.p + (size_t)r0 * qa_ld;
-    float* sar = sa.p + r0;
-    LLM_HIP_RET(launch_layernorm_quant(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
-                                       qar, sar, st, 1));
-    g.A = qar; g.sa = sar; g.sw = sw_qkv.p + (size_t)l * 3 * hid;
+    LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
+                                       static_cast<int8_t*>(R.act), R.sa, st, 1));
+    g.sa = R.sa; g.sw = sw_qkv.p + (size_t)l * 3 * hid;
   } else {
-    uint16_t* a16r = a16.p + (size_t)r0 * qa_ld;
-    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, a16r, st, 1));
-    g.A = a16r;
+    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, R.act, st, 1));
   }
   return weight_gemm(g, st);
 }
 
-int llm_decoder::layer_attn(int l, hipStream_t st, const MicroBatch& mb) {
-  const int r0 = mb.r0, B = mb.n;
+int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
-  view.page_table += (size_t)r0 * H * view.max_tiles;  // rows of this micro-batch
-  view.num_beams -= r0;
+  view.page_table += (size_t)R.table_row0 * H * view.max_tiles;  // rows of this micro-batch
+  view.num_beams -= R.table_row0;
   // the split merge also produces the o_proj input (packed int8 + scale, or fp16)
   PaRowOutputs ro;
   ro.pack = 1;
   if (wdtype == LLM_I8) {
-    ro.q = qa.p + (size_t)r0 * qa_ld;
-    ro.inv_scale = sa.p + r0;
+    ro.q = static_cast<int8_t*>(R.act);
+    ro.inv_scale = R.sa;
   } else {
-    ro.out16 = a16.p + (size_t)r0 * qa_ld;
+    ro.out16 = R.act;
   }
-  return pa_decode_internal(&view, qkv.p + (size_t)r0 * hid, hid, o.p + (size_t)r0 * hid, nullptr,
-                            ctx.p + r0, B, H, D, cfg.max_seq_len, cfg.attn_scale, pps, mb.attn_ws,
-                            attn_ws_bytes, st, &ro, r0 % row_group == 0 ? row_group : 1);
+  return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
+                            cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
+                            R.row_group);
 }
 
-int llm_decoder::layer_post(int l, hipStream_t st, const MicroBatch& mb) {
-  const int r0 = mb.r0, B = mb.n;
+int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   const size_t lh = (size_t)l * hid;
-  float* xr = x.p + (size_t)r0 * hid;
-  float* h1r = h1.p + (size_t)r0 * inter;
   const bool i8 = wdtype == LLM_I8;
-  void* ar = i8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
-  float* sar = sa.p + r0;
   WeightGemm g;
   g.dtype = wdtype;
   g.a_packed = 1;
-  g.A = ar;
-  g.M = B;
+  g.A = R.act;
+  g.M = R.n;
   // o_proj: input produced (packed) by the attention merge
-  g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = xr;
-  if (i8) { g.sa = sar; g.sw = sw_o.p + lh; }
+  g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = R.x;
+  if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
   RET_IF(weight_gemm(g, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
   if (i8)
-    LLM_HIP_RET(launch_layernorm_quant(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
-                                       static_cast<int8_t*>(ar), sar, st, 1));
+    LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
+                                       static_cast<int8_t*>(R.act), R.sa, st, 1));
   else
-    LLM_HIP_RET(launch_layernorm_f16(xr, B, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, ar, st, 1));
-  g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid; g.C = h1r;
+    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, R.act, st, 1));
+  g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid; g.C = R.h1;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
   if (i8) g.sw = sw1.p + (size_t)l * inter;
   RET_IF(weight_gemm(g, st));
   // quantise h1 -> mlp_fc2 (+b2)
   if (i8)
-    LLM_HIP_RET(launch_quantize_rows(h1r, B, inter, static_cast<int8_t*>(ar), sar, st, 1));
+    LLM_HIP_RET(launch_quantize_rows(R.h1, R.n, inter, static_cast<int8_t*>(R.act), R.sa, st, 1));
   else
-    LLM_HIP_RET(launch_to_f16(h1r, (size_t)B * inter, ar, st, inter));
-  g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = xr;
+    LLM_HIP_RET(launch_to_f16(R.h1, (size_t)R.n * inter, R.act, st, inter));
+  g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
   return weight_gemm(g, st);
 }
 
-int llm_decoder::step_head(hipStream_t st, const MicroBatch& mb) {
-  return launch_embed(emb.p, tokens.p + mb.r0, mb.n, hid, V, x.p + (size_t)mb.r0 * hid, st) ==
-                 hipSuccess
+// Rows r0 .. r0 + n - 1 of the decode-step buffers.
+Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
+  Rows R;
+  R.n = n;
+  R.x = x.p + (size_t)r0 * hid;
+  R.q = qkv.p + (size_t)r0 * hid;
+  R.o = o.p + (size_t)r0 * hid;
+  R.h1 = h1.p + (size_t)r0 * inter;
+  R.act = wdtype == LLM_I8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
+  R.sa = sa.p + r0;
+  R.pos = pos.p + r0;
+  R.ctx = ctx.p + r0;
+  R.table_row0 = r0;
+  R.row_group = r0 % row_group == 0 ? row_group : 1;
+  R.attn_ws = ws;
+  R.attn_ws_bytes = attn_ws_bytes;
+  return R;
+}
+
+int llm_decoder::step_head(hipStream_t st, int r0, int n) {
+  return launch_embed(emb.p, tokens.p + r0, n, hid, V, x.p + (size_t)r0 * hid, st) == hipSuccess
              ? LLM_OK
              : fail(LLM_ERR_HIP, "embed launch");
 }
 
-int llm_decoder::step_tail(hipStream_t st, const MicroBatch& mb) {
-  const int r0 = mb.r0;
+int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
   float* lg = logits.p + (size_t)r0 * V;
-  RET_IF(lm_head(x.p + (size_t)r0 * hid, emb.p, lg, mb.n, V, hid, st));
+  RET_IF(lm_head(x.p + (size_t)r0 * hid, emb.p, lg, n, V, hid, st));
   if (temperature > 0.f && top_k != 1)  // draw counter = the row's position
-    LLM_HIP_RET(launch_sample(lg, mb.n, r0, V, temperature, top_k, top_p, sample_seed, pos.p + r0,
+    LLM_HIP_RET(launch_sample(lg, n, r0, V, temperature, top_k, top_p, sample_seed, pos.p + r0,
                               tokens.p + r0, st));
   else
-    LLM_HIP_RET(launch_argmax(lg, mb.n, V, tokens.p + r0, nullptr, 0, st));  // next tokens in place
-  LLM_HIP_RET(launch_advance(pos.p + r0, ctx.p + r0, mb.n, st));
+    LLM_HIP_RET(launch_argmax(lg, n, V, tokens.p + r0, nullptr, 0, st));  // next tokens in place
+  LLM_HIP_RET(launch_advance(pos.p + r0, ctx.p + r0, n, st));
   return LLM_OK;
 }
 
@@ -430,35 +469,23 @@ int llm_decoder::step_tail(hipStream_t st, const MicroBatch& mb) {
 // (LayerNorm, quantisation, weight GEMMs, KV append, split merge) runs beside
 // it instead of between attention launches.
 int llm_decoder::enqueue_step(hipStream_t st) {
-  const int nmb = (batch >= 2 && microbatches >= 2) ? 2 : 1;
-  MicroBatch mbs[2];
-  if (nmb == 1) {
-    mbs[0] = {0, batch, attn_ws.p};
-    RET_IF(step_head(st, mbs[0]));
-    for (int l = 0; l < L; ++l) {
-      RET_IF(layer_pre(l, st, mbs[0]));
-      RET_IF(layer_attn(l, st, mbs[0]));
-      RET_IF(layer_post(l, st, mbs[0]));
-    }
-    return step_tail(st, mbs[0]);
-  }
   const int h0 = ((batch + 1) / 2 + 15) / 16 * 16;  // packed-A tiles are 16 rows
-  if (h0 >= batch) {
-    mbs[0] = {0, batch, attn_ws.p};
-    RET_IF(step_head(st, mbs[0]));
+  if (microbatches < 2 || batch < 2 || h0 >= batch) {
+    const Rows R = step_rows(0, batch, attn_ws.p);
+    RET_IF(step_head(st, 0, batch));
     for (int l = 0; l < L; ++l) {
-      RET_IF(layer_pre(l, st, mbs[0]));
-      RET_IF(layer_attn(l, st, mbs[0]));
-      RET_IF(layer_post(l, st, mbs[0]));
+      RET_IF(layer_pre(l, st, R));
+      RET_IF(layer_attn(l, st, R));
+      RET_IF(layer_post(l, st, R));
     }
-    return step_tail(st, mbs[0]);
+    return step_tail(st, 0, batch);
   }
-  mbs[0] = {0, h0, attn_ws.p};
-  mbs[1] = {h0, batch - h0, attn_ws2.p};
+  const Rows mbs[2] = {step_rows(0, h0, attn_ws.p), step_rows(h0, batch - h0, attn_ws2.p)};
+  const int r0s[2] = {0, h0};
   hipStream_t S[2] = {st, stream2};
   LLM_HIP_RET(hipEventRecord(ev_fork, st));
   LLM_HIP_RET(hipStreamWaitEvent(stream2, ev_fork, 0));
-  for (int j = 0; j < 2; ++j) RET_IF(step_head(S[j], mbs[j]));
+  for (int j = 0; j < 2; ++j) RET_IF(step_head(S[j], r0s[j], mbs[j].n));
   for (int l = 0; l < L; ++l) {
     for (int j = 0; j < 2; ++j) {
       RET_IF(layer_pre(l, S[j], mbs[j]));
@@ -472,7 +499,7 @@ int llm_decoder::enqueue_step(hipStream_t st) {
       RET_IF(layer_post(l, S[j], mbs[j]));
     }
   }
-  for (int j = 0; j < 2; ++j) RET_IF(step_tail(S[j], mbs[j]));
+  for (int j = 0; j < 2; ++j) RET_IF(step_tail(S[j], r0s[j], mbs[j].n));
   LLM_HIP_RET(hipEventRecord(ev_join, stream2));
   LLM_HIP_RET(hipStreamWaitEvent(st, ev_join, 0));
   return LLM_OK;
@@ -526,6 +553,84 @@ int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t
     LLM_HIP_RET(hipMemcpyAsync(next_host, tokens.p, sizeof(int32_t) * batch,
                                hipMemcpyDeviceToHost, st));
     LLM_HIP_RET(hipStreamSynchronize(st));
+  }
+  return LLM_OK;
+}
+
+// Chunked prefill of `n` prompt tokens of active row `row` (the reference's
+// is_prefill pass, attention/attention_cuda.hpp:21): the chunk's tokens are
+// the rows of one layer pass — M = chunk-size weight GEMMs, the K/V of every
+// token appended to the row's pages by the qkv epilogue, and causal attention
+// through the same paged decode kernel (token i of the chunk attends to the
+// row's positions < p0 + i + 1 via beam_ids = row, context_lens = p0 + i + 1).
+// The last token's logits pick the row's next token (argmax / sampling), so
+// decode steps continue from the prompt.
+int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
+  LLM_REQUIRE(weights_ready, "prefill: weights not loaded");
+  LLM_REQUIRE(row >= 0 && row < batch, "prefill: row is not active");
+  LLM_REQUIRE(n >= 1 && toks, "prefill: need >= 1 token");
+  LLM_REQUIRE(h_pos[row] + n < cfg.max_seq_len, "prefill: prompt exceeds max_seq_len");
+  for (int i = 0; i < n; ++i) LLM_REQUIRE(toks[i] >= 0 && toks[i] < V, "prefill: token id out of range");
+  const int C = std::min(n, kPrefillChunk);
+  if (C > pf_cap) {
+    const size_t C16 = ((size_t)C + 15) / 16 * 16;
+    RET_IF(px.alloc((size_t)C * hid));
+    RET_IF(pq.alloc((size_t)C * hid));
+    RET_IF(po.alloc((size_t)C * hid));
+    RET_IF(ph1.alloc((size_t)C * inter));
+    RET_IF(psa.alloc((size_t)C));
+    RET_IF(pact.alloc(C16 * std::max(hid, inter) * (wdtype == LLM_I8 ? 1 : 2)));
+    RET_IF(pmeta.alloc((size_t)4 * C));
+    pws_bytes = 16;
+    for (int b = 1; b <= C; ++b)
+      pws_bytes = std::max(pws_bytes, pa_decode_workspace_bytes(b, H, D, max_tiles, 0));
+    RET_IF(pws.alloc(pws_bytes));
+    pf_cap = C;
+  }
+  KvCache* k = kv_impl(kv);
+  std::vector<int32_t> meta((size_t)4 * C), pc(2);
+  for (int c0 = 0; c0 < n; c0 += C) {
+    const int m = std::min(C, n - c0);
+    const int p0 = h_pos[row];
+    {
+      std::lock_guard<std::mutex> gk(k->mu);
+      for (int t = p0; t < p0 + m; t = (t / TS + 1) * TS) RET_IF(k->prepare_append(row, t));
+      RET_IF(k->sync(st));
+    }
+    for (int i = 0; i < m; ++i) {
+      meta[i] = p0 + i;
+      meta[C + i] = p0 + i + 1;
+      meta[2 * C + i] = row;
+      meta[3 * C + i] = toks[c0 + i];
+    }
+    LLM_HIP_RET(hipMemcpyAsync(pmeta.p, meta.data(), meta.size() * sizeof(int32_t),
+                               hipMemcpyHostToDevice, st));
+    Rows R;
+    R.n = m;
+    R.x = px.p; R.q = pq.p; R.o = po.p; R.h1 = ph1.p; R.act = pact.p; R.sa = psa.p;
+    R.pos = pmeta.p; R.ctx = pmeta.p + C; R.beam_rows = pmeta.p + 2 * C;
+    R.attn_ws = pws.p; R.attn_ws_bytes = pws_bytes;
+    LLM_HIP_RET(launch_embed(emb.p, pmeta.p + 3 * C, m, hid, V, px.p, st));
+    for (int l = 0; l < L; ++l) {
+      RET_IF(layer_pre(l, st, R));
+      RET_IF(layer_attn(l, st, R));
+      RET_IF(layer_post(l, st, R));
+    }
+    h_pos[row] = p0 + m;
+    if (c0 + m == n) {  // last token: logits -> the row's next token, decode state
+      float* lg = logits.p + (size_t)row * V;
+      RET_IF(lm_head(px.p + (size_t)(m - 1) * hid, emb.p, lg, 1, V, hid, st));
+      if (temperature > 0.f && top_k != 1)
+        LLM_HIP_RET(launch_sample(lg, 1, row, V, temperature, top_k, top_p, sample_seed,
+                                  pmeta.p + (m - 1), tokens.p + row, st));
+      else
+        LLM_HIP_RET(launch_argmax(lg, 1, V, tokens.p + row, nullptr, 0, st));
+      pc[0] = p0 + m;
+      pc[1] = p0 + m + 1;
+      LLM_HIP_RET(hipMemcpyAsync(pos.p + row, &pc[0], sizeof(int32_t), hipMemcpyHostToDevice, st));
+      LLM_HIP_RET(hipMemcpyAsync(ctx.p + row, &pc[1], sizeof(int32_t), hipMemcpyHostToDevice, st));
+    }
+    LLM_HIP_RET(hipStreamSynchronize(st));  // meta / pc staging reused next chunk
   }
   return LLM_OK;
 }
@@ -609,6 +714,12 @@ extern "C" int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_wi
   return LLM_OK;
 }
 
+extern "C" int llm_decoder_prefill(llm_decoder* d, int row, const int32_t* tokens, int n) {
+  LLM_REQUIRE(d, "llm_decoder_prefill: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  return d->prefill(row, tokens, n, d->stream);
+}
+
 extern "C" int llm_decoder_set_sampling(llm_decoder* d, float temperature, int top_k, float top_p,
                                         uint64_t seed) {
   LLM_REQUIRE(d, "llm_decoder_set_sampling: NULL");
@@ -666,16 +777,17 @@ extern "C" int llm_decoder_generate(llm_decoder* d, const int32_t* prompts,
               "llm_decoder_generate: prompt + max_gen_len exceeds max_seq_len");
   LLM_HIP_RET(hipStreamSynchronize(d->stream));
   RET_IF(reset_rows(d, batch, 0));
-  const int steps = max_len + max_gen_len - 1;
+  // every prompt but its last token goes through chunked prefill; decode steps
+  // then run all rows in lockstep, each at its own position
+  for (int b = 0; b < batch; ++b)
+    if (prompt_lens[b] > 1)
+      RET_IF(d->prefill(b, prompts + (size_t)b * prompt_stride, prompt_lens[b] - 1, d->stream));
   std::vector<int32_t> tok(batch), next(batch);
-  for (int s = 0; s < steps; ++s) {
+  for (int s = 0; s < max_gen_len; ++s) {
     for (int b = 0; b < batch; ++b)
-      tok[b] = s < prompt_lens[b] ? prompts[(size_t)b * prompt_stride + s] : next[b];
+      tok[b] = s == 0 ? prompts[(size_t)b * prompt_stride + prompt_lens[b] - 1] : next[b];
     RET_IF(d->run_step(tok.data(), nullptr, next.data(), d->stream));
-    for (int b = 0; b < batch; ++b) {
-      const int gi = s - (prompt_lens[b] - 1);
-      if (gi >= 0 && gi < max_gen_len) out[(size_t)b * max_gen_len + gi] = next[b];
-    }
+    for (int b = 0; b < batch; ++b) out[(size_t)b * max_gen_len + s] = next[b];
   }
   return LLM_OK;
 }

@@ -35,6 +35,7 @@ namespace llm {
 struct KvAppend {
   const int32_t* pos;
   const int32_t* page_table;  // [num_beams][H][max_tiles] of this layer (row offset applied)
+  const int32_t* rows;        // page-table row of GEMM row m (NULL: m) — prefill chunks
   _Float16* k_pool;
   _Float16* v_pool;
   int num_beams, max_tiles, TS, num_pages, H, D;
@@ -286,14 +287,15 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     if constexpr (KIND != GemmKind::LMHEAD) {
       const KvAppend& kv = a.kv;
       const int hid = kv.H * kv.D;
-      if (kv.k_pool && n >= hid && m < kv.num_beams) {
+      const int br = kv.rows ? kv.rows[m] : m;
+      if (kv.k_pool && n >= hid && br >= 0 && br < kv.num_beams) {
         const int which = n >= 2 * hid;  // 0: K, 1: V
         const int i = n - hid * (1 + which);
         const int h = i / kv.D, d = i - h * kv.D;
         const int p = kv.pos[m];
         const int tile = p / kv.TS;
         if (tile < kv.max_tiles) {
-          const int page = kv.page_table[((size_t)m * kv.H + h) * kv.max_tiles + tile];
+          const int page = kv.page_table[((size_t)br * kv.H + h) * kv.max_tiles + tile];
           if (page >= 0 && page < kv.num_pages) {
             const size_t off = ((size_t)page * kv.TS + (p - tile * kv.TS)) * kv.D + d;
             (which ? kv.v_pool : kv.k_pool)[off] = (_Float16)y;
@@ -487,7 +489,7 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");
-    a.kv = KvAppend{kv.pos, kv.page_table, static_cast<_Float16*>(kv.k_pool),
+    a.kv = KvAppend{kv.pos, kv.page_table, kv.rows, static_cast<_Float16*>(kv.k_pool),
                     static_cast<_Float16*>(kv.v_pool), kv.num_beams, kv.max_tiles, kv.page_size,
                     kv.num_pages, kv.H, kv.D};
   }

@@ -14,9 +14,10 @@ namespace llm {
 struct KvAppendView {
   const int32_t* pos;
   const int32_t* page_table;
+  const int32_t* rows;  // page-table row of GEMM row m (NULL: row m)
   void* k_pool;
   void* v_pool;
-  int num_beams, max_tiles, page_size, num_pages, H, D;
+  int num_beams = 0, max_tiles = 0, page_size = 0, num_pages = 0, H = 0, D = 0;
 };
 
 // One decode weight GEMM (decoder-internal form of i8_gemm / f16_gemm):

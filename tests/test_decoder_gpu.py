@@ -366,3 +366,51 @@ def test_decoder_device_sampling(gpu, oracle):
     nxt = dec.step(toks, logits_ptr=logits.data_ptr(), want_next=True)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(np.asarray(nxt), logits.cpu().numpy().argmax(1))
+
+
+def test_prefill_matches_token_by_token(gpu, oracle):
+    """Chunked prefill (one layer pass per <= 512-token chunk, causal paged
+    attention per token) leaves the same KV and state as feeding the prompt one
+    token per decode step: the step after the prompt gives the same logits
+    (1e-4 rel: only the attention split order differs) and the same next ids;
+    prompts of 600 (two chunks) and 37 tokens, ragged."""
+    torch = _torch()
+    w = _int8_model(oracle, L=2, H=4, D=64, V=500, S=1024, seed=12)
+    V = w["cfg"]["V"]
+    rng = np.random.default_rng(3)
+    prompts = [rng.integers(0, V, 600).tolist(), rng.integers(0, V, 37).tolist()]
+    lens = [len(p) for p in prompts]
+
+    # A: token by token, teacher forced; rows stop advancing once their prompt is in
+    a = _make_gpu_decoder(w, max_batch=2)
+    a.begin_synthetic(2, 0, 0, False)
+    la = torch.empty((2, V), device="cuda")
+    logits_a = [None, None]
+    for s in range(max(lens)):
+        toks = [p[min(s, len(p) - 1)] for p in prompts]
+        if s >= lens[1]:  # row 1 is done: keep it separate (decode in its own decoder)
+            break
+        a.step(toks, logits_ptr=la.data_ptr())
+    torch.cuda.synchronize()
+    logits_a[1] = la[1].cpu().numpy().copy()
+    a1 = _make_gpu_decoder(w, max_batch=1)
+    a1.begin_synthetic(1, 0, 0, False)
+    l1 = torch.empty((1, V), device="cuda")
+    for t in prompts[0]:
+        a1.step([t], logits_ptr=l1.data_ptr())
+    torch.cuda.synchronize()
+    logits_a[0] = l1[0].cpu().numpy().copy()
+
+    # B: prefill all but the last prompt token, then one decode step with it
+    b = _make_gpu_decoder(w, max_batch=2)
+    b.begin_synthetic(2, 0, 0, False)
+    for r, p in enumerate(prompts):
+        b.prefill(r, p[:-1])
+    lb = torch.empty((2, V), device="cuda")
+    nxt = b.step([p[-1] for p in prompts], logits_ptr=lb.data_ptr(), want_next=True)
+    torch.cuda.synchronize()
+    lb = lb.cpu().numpy()
+    for r in range(2):
+        assert b.context_len(r) == lens[r]  # tokens now in the row's KV
+        assert rel_err(lb[r], logits_a[r]) < 1e-4, (r, rel_err(lb[r], logits_a[r]))
+        assert nxt[r] == int(np.argmax(logits_a[r]))
