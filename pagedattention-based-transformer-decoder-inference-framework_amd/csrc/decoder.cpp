@@ -109,6 +109,7 @@ struct llm_decoder {
 
   // micro-batch overlap (see enqueue_step)
   int microbatches = 1;
+  int mb_attn_waves = 0;  // LLM_MB_ATTN_WAVES: attention waves per SIMD under overlap
   int row_group = 1;  // beam width of llm_decoder_begin_beams (beam-aware attention)
   // sampling (llm_decoder_set_sampling); greedy argmax by default, as the
   // reference's sample_from_logits (decoder/cuda_decoder.cu:7-14)
@@ -195,12 +196,17 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
                                 pa_decode_workspace_bytes(b, d->H, d->D, d->max_tiles, 0));
   RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
   d->qa_ld = std::max(hid, inter);
-  // micro-batch overlap: LLM_MICROBATCHES=1|2 (default 1: measured slower at C3,
-  // 3596 vs 3623 tok/s — the glue kernels slow down beside a saturating scan),
-  // LLM_MB_PINGPONG=0|1, LLM_GRAPH=0|1 (eager launches, for profiling)
+  // micro-batch overlap (enqueue_step), off by default: LLM_MICROBATCHES=1|2,
+  // LLM_MB_PINGPONG=0|1, LLM_MB_ATTN_WAVES=n (lean attention under overlap),
+  // LLM_GRAPH=0|1 (eager launches, for profiling).  Measured at C3 (tok/s):
+  // one batch 3607-3621; two free-running halves 3672-3674 (+1.5 %, within
+  // box-to-box spread, and 7 % slower under rocprofv3's kernel trace);
+  // ping-pong attention 3156-3592 — the glue kernels slow 4-8x beside a
+  // saturating KV scan, so the overlap does not pay on this path.
   d->microbatches = env_int("LLM_MICROBATCHES", 1);
-  d->pingpong = env_int("LLM_MB_PINGPONG", 1) != 0;
+  d->pingpong = env_int("LLM_MB_PINGPONG", 0) != 0;
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
+  d->mb_attn_waves = env_int("LLM_MB_ATTN_WAVES", 0);
   if (d->microbatches >= 2 && B >= 2) {
     LLM_HIP_RET(hipStreamCreateWithFlags(&d->stream2, hipStreamNonBlocking));
     LLM_HIP_RET(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
@@ -329,6 +335,7 @@ struct Rows {
   const int32_t* beam_rows = nullptr;  // page-table row per row; NULL: table_row0 + m
   int table_row0 = 0;
   int row_group = 1;
+  int attn_waves_per_simd = 0;  // > 0: lean attention leaving CU room (micro-batch overlap)
   uint8_t* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
 };
@@ -389,7 +396,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   }
   return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
-                            R.row_group);
+                            R.row_group, R.attn_waves_per_simd);
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
@@ -480,7 +487,8 @@ int llm_decoder::enqueue_step(hipStream_t st) {
     }
     return step_tail(st, 0, batch);
   }
-  const Rows mbs[2] = {step_rows(0, h0, attn_ws.p), step_rows(h0, batch - h0, attn_ws2.p)};
+  Rows mbs[2] = {step_rows(0, h0, attn_ws.p), step_rows(h0, batch - h0, attn_ws2.p)};
+  mbs[0].attn_waves_per_simd = mbs[1].attn_waves_per_simd = mb_attn_waves;
   const int r0s[2] = {0, h0};
   hipStream_t S[2] = {st, stream2};
   LLM_HIP_RET(hipEventRecord(ev_fork, st));

@@ -90,7 +90,7 @@ constexpr int kKvLoadAux = 2;
 // the current one is computed; 1: latency hidden by occupancy alone).
 // MIN_WAVES > 0 asks the compiler for that many waves per SIMD.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
-          int STAGES = 2, int MIN_WAVES = 0>
+          int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
   constexpr int LPT = D / 8;
@@ -189,6 +189,13 @@ void pa_split_kernel(PaSplitArgs a) {
   };
 
   auto compute = [&](const u32x4 (&kk)[NR], const u32x4 (&vv)[NR], int p0) {
+    if constexpr (LOAD_ONLY) {  // tuning: the same stream with a trivial consumer
+      uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) x ^= kk[i][0] ^ kk[i][3] ^ vv[i][1] ^ vv[i][2];
+      acc[0] += (float)(x & 1u);
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = p0 + u;
@@ -449,22 +456,32 @@ long long resident_waves() {
   return cached;
 }
 
+// lean = the low-register form (one 8 KiB register stage, 8 waves per SIMD
+// requested): same stream rate measured (scripts/tune_attention.py variant 6
+// vs 1), used when the launch must leave CU room for kernels running beside
+// it (micro-batch overlap).
 template <int D, int TS>
-hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st) {
+hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_t st) {
   const int waves = ((a.B + a.group - 1) / a.group) * a.group * a.H * a.nsplit;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (direct)
+  if (lean) {
+    if (direct)
+      hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
+  } else if (direct) {
     hipLaunchKernelGGL((pa_split_kernel<D, TS, true>), grid, block, 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false>), grid, block, 0, st, a);
+  }
   return hipGetLastError();
 }
 
 template <int D>
-hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, hipStream_t st) {
+hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, bool lean, hipStream_t st) {
   switch (TS) {
-    case 16: return launch_split<D, 16>(a, direct, st);
-    case 32: return launch_split<D, 32>(a, direct, st);
+    case 16: return launch_split<D, 16>(a, direct, lean, st);
+    case 32: return launch_split<D, 32>(a, direct, lean, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -553,7 +570,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                             int D, int T, float sm_scale, int pages_per_split, void* workspace,
                             size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows,
-                            int row_group) {
+                            int row_group, int waves_per_simd) {
   LLM_REQUIRE(kv != nullptr, "pa_decode: kv view is NULL");
   LLM_REQUIRE(B >= 0 && H > 0 && D > 0 && T >= 0, "pa_decode: bad B/H/D/T");
   if (B == 0) return LLM_OK;
@@ -577,8 +594,23 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // tiles at or past max_tiles have no page-table entry: they are missing (masked)
   const int ntiles_max = std::max(1, std::min((T + TS - 1) / TS, kv->max_tiles));
   const int pps_fixed = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps) : 0;
-  const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed,
-                                   pps_fixed > 0 ? 0 : resident_waves_for(D, TS));
+  // waves_per_simd > 0: lean kernel, splits sized for that many waves per SIMD
+  const bool lean = waves_per_simd > 0;
+  long long resident = 0;
+  if (pps_fixed <= 0) {
+    if (lean) {
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        cus = 256;
+      }
+      resident = (long long)cus * 4 * std::min(waves_per_simd, 8);
+    } else {
+      resident = resident_waves_for(D, TS);
+    }
+  }
+  const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
   const bool direct = nsplit <= 1;
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
 
@@ -610,10 +642,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   hipError_t e;
   switch (D) {
-    case 32: e = dispatch_ts<32>(a, TS, direct, st); break;
-    case 64: e = dispatch_ts<64>(a, TS, direct, st); break;
-    case 128: e = dispatch_ts<128>(a, TS, direct, st); break;
-    default: e = dispatch_ts<256>(a, TS, direct, st); break;
+    case 32: e = dispatch_ts<32>(a, TS, direct, lean, st); break;
+    case 64: e = dispatch_ts<64>(a, TS, direct, lean, st); break;
+    case 128: e = dispatch_ts<128>(a, TS, direct, lean, st); break;
+    default: e = dispatch_ts<256>(a, TS, direct, lean, st); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
   if (row_out && !direct) {
@@ -698,6 +730,9 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
     case 7: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 1, 4>), grid, block, 0, st, a); break;
     case 8: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 2, 4>), grid, block, 0, st, a); break;
     case 9: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 1, 6>), grid, block, 0, st, a); break;
+    case 10: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 2, 0, true>), grid, block, 0, st, a); break;
+    case 11: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 1, 8, true>), grid, block, 0, st, a); break;
+    case 12: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 2, 2, 0, true>), grid, block, 0, st, a); break;
     default: return fail(LLM_ERR_INVALID, "pa_decode_tune: variant");
   }
   LLM_HIP_RET(hipGetLastError());

@@ -23,7 +23,8 @@ int pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float
                        const int32_t* beam_ids, const int32_t* context_lens, int B, int H, int D,
                        int T, float sm_scale, int pages_per_split, void* workspace,
                        size_t workspace_bytes, hipStream_t st,
-                       const PaRowOutputs* rows = nullptr, int row_group = 1);
+                       const PaRowOutputs* rows = nullptr, int row_group = 1,
+                       int waves_per_simd = 0);
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 
 }  // namespace llm

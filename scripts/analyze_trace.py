@@ -10,14 +10,12 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
-emb = [i for i, r in enumerate(rows) if "embed_kernel" in r["Kernel_Name"]]
-adv = [i for i, r in enumerate(rows) if "advance_kernel" in r["Kernel_Name"]]
-# the last step: its embeds start within 1 ms of each other
-first = emb[-1]
-while first > 0 and emb.index(first) > 0 and rows[first]["s"] - rows[emb[emb.index(first) - 1]]["s"] < 1_000_000:
-    first = emb[emb.index(first) - 1]
-last_adv = adv[-1]
-step = [r for r in rows[first:last_adv + 1]]
+adv = [r for r in rows if "advance_kernel" in r["Kernel_Name"]]
+nmb = len({r["Queue_Id"] for r in adv}) or 1  # micro-batches (one advance each per step)
+adv.sort(key=lambda r: r["e"])
+t_end = adv[-1]["e"]
+t_beg = adv[-1 - nmb]["e"] if len(adv) > nmb else rows[0]["s"]
+step = [r for r in rows if r["s"] >= t_beg and r["e"] <= t_end]
 # include trailing advance kernels
 t0 = step[0]["s"]
 t1 = max(r["e"] for r in step)

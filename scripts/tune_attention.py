@@ -23,15 +23,23 @@ ap.add_argument("--variants", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5])
 ap.add_argument("--pps", type=int, nargs="*", default=[64])
 ap.add_argument("--T", type=int, default=8192)
 ap.add_argument("--B", type=int, default=64)
+ap.add_argument("--interleave", action="store_true",
+                help="K and V of a page adjacent (one 2*page pool, K at even, V at odd pages)")
 args = ap.parse_args()
 B, H, D, T, ts = args.B, 16, 128, args.T, 16
 nt = (T + ts - 1) // ts
 num_pages = B * H * nt
 g = torch.Generator(device="cuda").manual_seed(0)
-kp = (torch.randn((num_pages, ts, D), generator=g, device="cuda") * D ** -0.25).half()
-vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
-q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
-pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
+if args.interleave:
+    kv = torch.randn((2 * num_pages, ts, D), generator=g, device="cuda").half()
+    kp, vp = kv[:-1], kv[1:]  # page p of kp = kv[p], of vp = kv[p + 1]
+    q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
+    pt = (2 * torch.randperm(num_pages, generator=g, device="cuda")).to(torch.int32).reshape(B, H, nt)
+else:
+    kp = (torch.randn((num_pages, ts, D), generator=g, device="cuda") * D ** -0.25).half()
+    vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
+    q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
+    pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
 lib = llm_capi.load()
 lib.pa_decode_tune.restype = ctypes.c_int
 lib.pa_decode_tune.argtypes = [ctypes.c_int, ctypes.POINTER(llm_capi.PaKvView), ctypes.c_void_p,
@@ -55,7 +63,7 @@ for r in range(args.rounds):
                                                   llm_capi.ptr(ws), ws_bytes, st))
             run()
             torch.cuda.synchronize()
-            if r == 0:
+            if r == 0 and v < 10:  # variants >= 10 are load-only ceilings
                 err = (out - ref).abs().max().item() / ref.abs().max().item()
                 assert err < 1e-5, (v, pps, err)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

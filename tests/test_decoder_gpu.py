@@ -414,3 +414,19 @@ def test_prefill_matches_token_by_token(gpu, oracle):
         assert b.context_len(r) == lens[r]  # tokens now in the row's KV
         assert rel_err(lb[r], logits_a[r]) < 1e-4, (r, rel_err(lb[r], logits_a[r]))
         assert nxt[r] == int(np.argmax(logits_a[r]))
+
+
+@pytest.mark.parametrize("mb,pp", [(1, 0), (2, 0), (2, 1)])
+def test_micro_batch_step_vs_oracle(gpu, oracle, monkeypatch, mb, pp):
+    """The step graph with the rows split into two micro-batches on two streams
+    (LLM_MICROBATCHES=2; 48 rows -> 32 + 16, 16-row packed-A boundary), free
+    running or with ping-pong attention ordering, against the oracle —
+    teacher forced, strict logits parity."""
+    from oracle.oracle import OracleDecoder
+    torch = _torch()
+    monkeypatch.setenv("LLM_MICROBATCHES", str(mb))
+    monkeypatch.setenv("LLM_MB_PINGPONG", str(pp))
+    w = _int8_model(oracle, L=2, H=4, D=64, V=600, S=32, seed=31)
+    dec = _make_gpu_decoder(w, max_batch=48)
+    odec = OracleDecoder(oracle, w, 48)
+    assert _teacher_forced(dec, odec, 5, 48, 600, seed=2) < LOGIT_TOL
