@@ -20,7 +20,8 @@ ap.add_argument("--hid", type=int, default=2048)
 args = ap.parse_args()
 lib = llm_capi.load()
 lib.i8_gemm_tune.restype = ctypes.c_int
-lib.i8_gemm_tune.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+lib.i8_gemm_tune.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                             ctypes.c_int,
                              ctypes.c_void_p, ctypes.c_void_p] + \
     [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 M, hid = args.M, args.hid
@@ -39,12 +40,13 @@ for name, K, N in shapes:
     C = torch.empty((M, N), device="cuda")
     ref = torch.empty_like(C)
     Ap = llm_capi.pack_weights(A.t().contiguous(), llm_capi.LLM_I8)  # A-fragment order
-    llm_capi.check(lib.i8_gemm_tune(1, 8, 0, A.data_ptr(), K, Wp.data_ptr(),
+    llm_capi.check(lib.i8_gemm_tune(1, 8, 0, 0, A.data_ptr(), K, Wp.data_ptr(),
                                     ref.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(), None))
-    for nt, ks, apk in [(1, 8, 0), (2, 8, 0), (1, 8, 1), (2, 8, 1), (1, 16, 1)]:
+    for nt, ks, apk, mr in [(1, 8, 1, 64), (2, 8, 1, 64), (1, 8, 1, 32), (2, 8, 1, 32),
+                            (1, 8, 1, 16), (1, 16, 1, 32)]:
         for _ in range(1):
             C.zero_()
-            llm_capi.check(lib.i8_gemm_tune(nt, ks, apk, (Ap if apk else A).data_ptr(), K,
+            llm_capi.check(lib.i8_gemm_tune(nt, ks, mr, apk, (Ap if apk else A).data_ptr(), K,
                                             Wp.data_ptr(),
                                             C.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(),
                                             None))
@@ -54,7 +56,7 @@ for name, K, N in shapes:
         with torch.cuda.graph(g, stream=s):
             st = torch.cuda.current_stream().cuda_stream
             for r in range(args.reps):
-                lib.i8_gemm_tune(nt, ks, apk, (Ap if apk else A).data_ptr(), K,
+                lib.i8_gemm_tune(nt, ks, mr, apk, (Ap if apk else A).data_ptr(), K,
                                  copies[r % 8].data_ptr(),
                                  C.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(),
                                  ctypes.c_void_p(st))
@@ -68,5 +70,5 @@ for name, K, N in shapes:
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / (3 * args.reps) * 1e-3
         byts = K * N
-        print(json.dumps({"gemm": name, "M": M, "K": K, "N": N, "NT": nt, "waves": ks, "a_packed": apk, "us": round(t * 1e6, 2),
+        print(json.dumps({"gemm": name, "M": M, "K": K, "N": N, "NT": nt, "waves": ks, "a_packed": apk, "mrows": mr, "us": round(t * 1e6, 2),
                           "weight_GBps": round(byts / t / 1e9, 1)}), flush=True)

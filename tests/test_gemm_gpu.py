@@ -65,7 +65,7 @@ def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
     import llm_capi
     lib = llm_capi.load()
     lib.i8_gemm_tune.restype = ctypes.c_int
-    lib.i8_gemm_tune.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+    lib.i8_gemm_tune.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                       ctypes.c_void_p] + [ctypes.c_int] * 3 + \
         [ctypes.c_void_p] * 3
     rng = np.random.default_rng(M + K + N + nt)
@@ -78,11 +78,12 @@ def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
     _, ref_C = oracle.i8_gemm(A, W, sa, sw, None, 0)
     dsa, dsw, dA = _dev(sa), _dev(sw), _dev(A)
     for packed, a_t in ((1, Ap), (0, dA)):
-        C = torch.full((M, N), float("nan"), device="cuda")
-        llm_capi.check(lib.i8_gemm_tune(nt, waves, packed, a_t.data_ptr(), K, Wp.data_ptr(),
-                                        C.data_ptr(), M, N, K, dsa.data_ptr(), dsw.data_ptr(),
-                                        None))
-        np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
+        for mrows in (0, 16, 32, 64):
+            C = torch.full((M, N), float("nan"), device="cuda")
+            llm_capi.check(lib.i8_gemm_tune(nt, waves, mrows, packed, a_t.data_ptr(), K,
+                                            Wp.data_ptr(), C.data_ptr(), M, N, K, dsa.data_ptr(),
+                                            dsw.data_ptr(), None))
+            np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
 
 
 @pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (64, 2048, 512), (3, 96, 48), (80, 256, 64)])
