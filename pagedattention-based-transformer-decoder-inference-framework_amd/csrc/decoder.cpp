@@ -85,6 +85,9 @@ struct llm_decoder {
 
   // activations / state
   DevBuf<float> x, qkv, o, h1, logits, sa;
+  DevBuf<float> lm_pv;    // [max_batch][lm_nwg] LM-head argmax partials
+  DevBuf<int32_t> lm_pi;
+  int lm_nwg = 0;
   DevBuf<int8_t> qa;
   DevBuf<uint16_t> a16;
   DevBuf<int32_t> tokens, pos, ctx;
@@ -131,6 +134,7 @@ struct llm_decoder {
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
   int step_tail(hipStream_t st, int r0, int n);
+  int next_tokens(const float* xr, int n, int r0, const int32_t* ctr, hipStream_t st);
   int enqueue_step(hipStream_t st);
   int run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host, hipStream_t st);
 
@@ -182,6 +186,9 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->o.alloc((size_t)B * hid));
   RET_IF(d->h1.alloc((size_t)B * inter));
   RET_IF(d->logits.alloc((size_t)B * d->V));
+  d->lm_nwg = lm_head_workgroups(d->V);
+  RET_IF(d->lm_pv.alloc((size_t)B * d->lm_nwg));
+  RET_IF(d->lm_pi.alloc((size_t)B * d->lm_nwg));
   RET_IF(d->sa.alloc((size_t)B));
   const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
   RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
@@ -451,6 +458,23 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
   return R;
 }
 
+// LM head + token choice for rows r0.. (x rows given): logits into the step's
+// logits buffer; greedy ids from the LM head's fused argmax partials, or a
+// device draw (sample_rows) with the rows' positions as draw counters.
+int llm_decoder::next_tokens(const float* xr, int n, int r0, const int32_t* ctr, hipStream_t st) {
+  float* lg = logits.p + (size_t)r0 * V;
+  const bool sample = temperature > 0.f && top_k != 1;
+  float* pv = lm_pv.p + (size_t)r0 * lm_nwg;
+  int32_t* pi = lm_pi.p + (size_t)r0 * lm_nwg;
+  LLM_HIP_RET(launch_lm_head(xr, emb.p, lg, n, V, hid, sample ? nullptr : pv, pi, st));
+  if (sample)
+    LLM_HIP_RET(launch_sample(lg, n, r0, V, temperature, top_k, top_p, sample_seed, ctr,
+                              tokens.p + r0, st));
+  else
+    LLM_HIP_RET(launch_argmax_partials(pv, pi, n, lm_nwg, tokens.p + r0, st));  // in place
+  return LLM_OK;
+}
+
 int llm_decoder::step_head(hipStream_t st, int r0, int n) {
   return launch_embed(emb.p, tokens.p + r0, n, hid, V, x.p + (size_t)r0 * hid, st) == hipSuccess
              ? LLM_OK
@@ -458,13 +482,7 @@ int llm_decoder::step_head(hipStream_t st, int r0, int n) {
 }
 
 int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
-  float* lg = logits.p + (size_t)r0 * V;
-  RET_IF(lm_head(x.p + (size_t)r0 * hid, emb.p, lg, n, V, hid, st));
-  if (temperature > 0.f && top_k != 1)  // draw counter = the row's position
-    LLM_HIP_RET(launch_sample(lg, n, r0, V, temperature, top_k, top_p, sample_seed, pos.p + r0,
-                              tokens.p + r0, st));
-  else
-    LLM_HIP_RET(launch_argmax(lg, n, V, tokens.p + r0, nullptr, 0, st));  // next tokens in place
+  RET_IF(next_tokens(x.p + (size_t)r0 * hid, n, r0, pos.p + r0, st));
   LLM_HIP_RET(launch_advance(pos.p + r0, ctx.p + r0, n, st));
   return LLM_OK;
 }
@@ -626,13 +644,7 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     }
     h_pos[row] = p0 + m;
     if (c0 + m == n) {  // last token: logits -> the row's next token, decode state
-      float* lg = logits.p + (size_t)row * V;
-      RET_IF(lm_head(px.p + (size_t)(m - 1) * hid, emb.p, lg, 1, V, hid, st));
-      if (temperature > 0.f && top_k != 1)
-        LLM_HIP_RET(launch_sample(lg, 1, row, V, temperature, top_k, top_p, sample_seed,
-                                  pmeta.p + (m - 1), tokens.p + row, st));
-      else
-        LLM_HIP_RET(launch_argmax(lg, 1, V, tokens.p + row, nullptr, 0, st));
+      RET_IF(next_tokens(px.p + (size_t)(m - 1) * hid, 1, row, pmeta.p + (m - 1), st));
       pc[0] = p0 + m;
       pc[1] = p0 + m + 1;
       LLM_HIP_RET(hipMemcpyAsync(pos.p + row, &pc[0], sizeof(int32_t), hipMemcpyHostToDevice, st));

@@ -5,7 +5,6 @@
 //             dnnl_matmul_int8, attention_cpu/dnnl_matmul_int8.cpp:7-75)
 //   f16_gemm: v_mfma_f32_16x16x32_f16 (CUDADecoder weights; MLP<T>::forward,
 //             decoder/mlp.hpp:23-41)
-//   lm_head : x . E^T with x split into fp16 hi + lo (two MFMAs per step)
 //
 // Decode GEMMs have M = rows in flight (<= 64 per block) and stream every
 // weight byte once: they are HBM-bound (128 op/B at M = 64 vs a ~625 op/B
@@ -61,9 +60,9 @@ struct GemmArgs {
 
 // k-steps per pipeline batch (two batches in flight): bounded by the VGPRs of
 // the A fragments (MT tiles, x2 for the fp32 LM-head A) held per k-step.
-template <int MT, int NA>
+template <int MT>
 constexpr int gemm_unroll() {
-  return MT * NA >= 8 ? 1 : (MT * NA >= 4 ? 2 : 4);
+  return MT >= 4 ? 2 : 4;
 }
 
 __device__ __forceinline__ float apply_act(float y, int act) {
@@ -72,7 +71,7 @@ __device__ __forceinline__ float apply_act(float y, int act) {
   return y;
 }
 
-enum class GemmKind { I8, F16, LMHEAD };
+enum class GemmKind { I8, F16 };
 
 template <GemmKind KIND>
 struct GemmTraits;
@@ -84,11 +83,6 @@ struct GemmTraits<GemmKind::I8> {
 template <>
 struct GemmTraits<GemmKind::F16> {
   static constexpr int KSTEP = 32, ESIZE = 2;
-  using acc_t = f32x4;
-};
-template <>
-struct GemmTraits<GemmKind::LMHEAD> {
-  static constexpr int KSTEP = 32, ESIZE = 4;  // A is fp32
   using acc_t = f32x4;
 };
 
@@ -103,8 +97,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   using Tr = GemmTraits<KIND>;
   using acc_t = typename Tr::acc_t;
   constexpr int KSTEP = Tr::KSTEP;
-  constexpr int NA = (KIND == GemmKind::LMHEAD) ? 2 : 1;  // 16-B A pieces per fragment
-  constexpr int kUnroll = gemm_unroll<MT, NA>();
+  constexpr int kUnroll = gemm_unroll<MT>();
   __shared__ __attribute__((aligned(16))) acc_t red[WAVES][MT * NT][64];
 
   const int lane = lane_id();
@@ -121,7 +114,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   // fragment is one contiguous 1 KiB block (one fully coalesced load).
   const int arow_lane = lane & 15;
   const int kgrp = lane >> 4;
-  const bool apk = KIND != GemmKind::LMHEAD && a.a_packed;
+  const bool apk = a.a_packed;
   const uint32_t a_bytes = apk ? (uint32_t)(((a.M + 15) / 16) * a.KS * 1024u)
                                : (uint32_t)((size_t)a.M * a.lda * Tr::ESIZE);
   const auto arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, (short)0, a_bytes, 0x00020000);
@@ -135,24 +128,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
                     : apk ? (uint32_t)((((m0 >> 4) + mt) * a.KS) * 1024u + lane * 16)
                           : (uint32_t)((size_t)row * a.lda * Tr::ESIZE);
   }
-  // B descriptor(s)
-  const uint8_t* bbase;
-  uint32_t b_bytes;
+  // B descriptor: this workgroup's NT packed column tiles
+  const uint8_t* bbase = a.B + (size_t)nt0 * a.KS * 1024;
+  const uint32_t b_bytes = (uint32_t)(min(NT, ntiles - nt0) * a.KS * 1024u);
   uint32_t b_lane_off[NT];
-  if constexpr (KIND == GemmKind::LMHEAD) {
-    bbase = a.B;  // E [N][K] fp16
-    b_bytes = (uint32_t)((size_t)a.N * a.K * 2);
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = (nt0 + j) * 16 + arow_lane;
-      b_lane_off[j] = n < a.N ? (uint32_t)((size_t)n * a.K * 2) + kgrp * 16 : 0xFFFFFFF0u;
-    }
-  } else {
-    bbase = a.B + (size_t)nt0 * a.KS * 1024;
-    b_bytes = (uint32_t)(min(NT, ntiles - nt0) * a.KS * 1024u);
-#pragma unroll
-    for (int j = 0; j < NT; ++j) b_lane_off[j] = (uint32_t)j * a.KS * 1024u + lane * 16;
-  }
+  for (int j = 0; j < NT; ++j) b_lane_off[j] = (uint32_t)j * a.KS * 1024u + lane * 16;
   const auto brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, b_bytes, 0x00020000);
 
   acc_t acc[MT][NT];
@@ -163,7 +144,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
 
   struct Batch {
     u32x4 b[kUnroll][NT];
-    u32x4 af[kUnroll][MT][NA];
+    u32x4 af[kUnroll][MT];
   };
   auto issue = [&](Batch& bt, int ks) {
 #pragma unroll
@@ -172,22 +153,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       const bool ok = kk < ks1;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        uint32_t boff;
-        if constexpr (KIND == GemmKind::LMHEAD)
-          boff = (ok && b_lane_off[j] != 0xFFFFFFF0u) ? b_lane_off[j] + (uint32_t)kk * KSTEP * 2
-                                                      : 0xFFFFFFF0u;
-        else
-          boff = ok ? b_lane_off[j] + (uint32_t)kk * 1024u : 0xFFFFFFF0u;
+        const uint32_t boff = ok ? b_lane_off[j] + (uint32_t)kk * 1024u : 0xFFFFFFF0u;
         bt.b[u][j] = __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff, 0, 2);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const uint32_t koff = (uint32_t)kk * a_kstride + a_kgrp_off;
         const uint32_t aoff = (ok && a_row_off[mt] != 0xFFFFFFF0u) ? a_row_off[mt] + koff : 0xFFFFFFF0u;
-#pragma unroll
-        for (int p = 0; p < NA; ++p)
-          bt.af[u][mt][p] = __builtin_amdgcn_raw_buffer_load_b128(
-              arsrc, aoff == 0xFFFFFFF0u ? aoff : aoff + 16 * p, 0, 0);
+        bt.af[u][mt] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff, 0, 0);
       }
     }
   };
@@ -200,31 +173,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
 #pragma unroll
           for (int j = 0; j < NT; ++j)
             acc[mt][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                __builtin_bit_cast(i32x4, bt.af[u][mt][0]), __builtin_bit_cast(i32x4, bt.b[u][j]),
+                __builtin_bit_cast(i32x4, bt.af[u][mt]), __builtin_bit_cast(i32x4, bt.b[u][j]),
                 acc[mt][j], 0, 0, 0);
         } else if constexpr (KIND == GemmKind::F16) {
 #pragma unroll
           for (int j = 0; j < NT; ++j)
             acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                __builtin_bit_cast(f16x8, bt.af[u][mt][0]), __builtin_bit_cast(f16x8, bt.b[u][j]),
+                __builtin_bit_cast(f16x8, bt.af[u][mt]), __builtin_bit_cast(f16x8, bt.b[u][j]),
                 acc[mt][j], 0, 0, 0);
-        } else {
-          const f32x4 x0 = __builtin_bit_cast(f32x4, bt.af[u][mt][0]);
-          const f32x4 x1 = __builtin_bit_cast(f32x4, bt.af[u][mt][NA - 1]);
-          f16x8 hi, lo;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            hi[e] = (_Float16)x0[e];
-            hi[4 + e] = (_Float16)x1[e];
-            lo[e] = (_Float16)(x0[e] - (float)hi[e]);
-            lo[4 + e] = (_Float16)(x1[e] - (float)hi[4 + e]);
-          }
-#pragma unroll
-          for (int j = 0; j < NT; ++j) {
-            const f16x8 bb = __builtin_bit_cast(f16x8, bt.b[u][j]);
-            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bb, acc[mt][j], 0, 0, 0);
-            acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bb, acc[mt][j], 0, 0, 0);
-          }
         }
       }
     }
@@ -284,7 +240,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     }
     y = apply_act(y, a.act);
     if (a.C && n < a.c_cols) a.C[(size_t)m * a.c_ld + n] = y;
-    if constexpr (KIND != GemmKind::LMHEAD) {
+    {
       const KvAppend& kv = a.kv;
       const int hid = kv.H * kv.D;
       const int br = kv.rows ? kv.rows[m] : m;
@@ -458,24 +414,6 @@ extern "C" int f16_gemm(const void* A, int lda, const void* W_packed, float* C, 
   return LLM_OK;
 }
 
-extern "C" int lm_head(const float* x, const void* E, float* logits, int M, int V, int K,
-                       void* stream) {
-  LLM_REQUIRE(M >= 0 && V > 0 && K > 0, "lm_head: bad M/V/K");
-  if (M == 0) return LLM_OK;
-  LLM_REQUIRE(x && E && logits, "lm_head: NULL operand");
-  LLM_REQUIRE(K % 32 == 0, "lm_head: K must be a multiple of 32");
-  LLM_REQUIRE((size_t)V * K * 2 < (1ull << 32) && (size_t)M * K * 4 < (1ull << 31),
-              "lm_head: operands too large for 32-bit offsets");
-  GemmArgs a{};
-  a.A = reinterpret_cast<const uint8_t*>(x);
-  a.lda = K;
-  a.B = static_cast<const uint8_t*>(E);
-  a.M = M; a.N = V; a.K = K; a.KS = K / 32;
-  a.C = logits; a.c_cols = V; a.c_ld = V;
-  hipError_t e = launch_gemm<GemmKind::LMHEAD>(a, as_stream(stream));
-  if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("lm_head: ") + hipGetErrorString(e));
-  return LLM_OK;
-}
 
 int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   LLM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0 && g.A && g.W_packed, "weight_gemm: bad arguments");
