@@ -75,6 +75,7 @@ struct llm_decoder {
 
   // weights
   DevBuf<uint16_t> emb;
+  DevBuf<uint8_t> emb_packed;  // LM-head copy of emb in B-fragment order
   DevBuf<float> ln1_g, ln1_b, ln2_g, ln2_b, b1, b2, sw_qkv, sw_o, sw1, sw2;
   DevBuf<uint8_t> wqkv, wo, w1, w2;  // packed, L consecutive blocks
   size_t sz_qkv = 0, sz_o = 0, sz_1 = 0, sz_2 = 0;
@@ -275,6 +276,9 @@ static int upload_common(llm_decoder* d, const uint16_t* emb, const float* ln1_g
                          const float* ln1_b, const float* ln2_g, const float* ln2_b) {
   const size_t Lh = (size_t)d->L * d->hid;
   RET_IF(upload(d->emb, emb, (size_t)d->V * d->hid, "emb"));
+  RET_IF(d->emb_packed.alloc(lm_head_packed_bytes(d->V, d->hid)));
+  LLM_HIP_RET(launch_lm_pack(d->emb.p, d->emb_packed.p, d->V, d->hid, nullptr));
+  LLM_HIP_RET(hipDeviceSynchronize());
   RET_IF(upload(d->ln1_g, ln1_g, Lh, "ln1_g"));
   RET_IF(upload(d->ln1_b, ln1_b, Lh, "ln1_b"));
   RET_IF(upload(d->ln2_g, ln2_g, Lh, "ln2_g"));
@@ -466,7 +470,7 @@ int llm_decoder::next_tokens(const float* xr, int n, int r0, const int32_t* ctr,
   const bool sample = temperature > 0.f && top_k != 1;
   float* pv = lm_pv.p + (size_t)r0 * lm_nwg;
   int32_t* pi = lm_pi.p + (size_t)r0 * lm_nwg;
-  LLM_HIP_RET(launch_lm_head(xr, emb.p, lg, n, V, hid, sample ? nullptr : pv, pi, st));
+  LLM_HIP_RET(launch_lm_head(xr, emb_packed.p, lg, n, V, hid, sample ? nullptr : pv, pi, st));
   if (sample)
     LLM_HIP_RET(launch_sample(lg, n, r0, V, temperature, top_k, top_p, sample_seed, ctr,
                               tokens.p + r0, st));

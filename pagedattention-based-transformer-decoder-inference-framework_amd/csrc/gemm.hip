@@ -312,12 +312,10 @@ hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hip
                  : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st);
 }
 
-// Waves per workgroup (they split K): 16 when the grid is short of one
-// workgroup per CU and K is deep, so each wave's dependent load chain halves.
-inline int pick_waves(const GemmArgs& a, int NT) {
-  const int wgs = (((a.N + 15) / 16 + NT - 1) / NT) * ((a.M + 63) / 64);
-  return (wgs < 256 && a.KS >= 64) ? 16 : 8;
-}
+// Waves per workgroup (they split K): 8.  The 16-wave form (1024 threads)
+// caps the kernel at 128 VGPRs and spills (scripts/kernel_resources.py); it is
+// kept for the tuning entry only.
+inline int pick_waves(const GemmArgs&, int) { return 8; }
 
 template <GemmKind KIND>
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t st, int nt_override = 0,

@@ -2,8 +2,11 @@
 // LM head the reference lacks: SURVEY Appendix A #20; argmax = sample_from_logits,
 // decoder/cuda_decoder.cu:7-14).
 //
-// x is fp32 [M][K] (M <= 64 per row block), E fp16 [V][K] row-major (the
-// embedding table itself, read once per step: V*K*2 bytes, HBM-bound).
+// x is fp32 [M][K] (M <= 64 per row block).  E fp16 [V][K] is the embedding
+// table; the LM head streams a copy repacked once at load time into MFMA
+// B-fragment order (lm_head_pack_embedding: one contiguous 1 KiB block per
+// (16 vocabulary rows, 32-wide k-step)), read once per step with fully
+// coalesced loads: V*K*2 bytes, HBM-bound.
 // To keep ~fp32 accuracy x is split into fp16 hi + lo and each E fragment
 // feeds two v_mfma_f32_16x16x32_f16.
 //
@@ -22,6 +25,9 @@
 #include "common.hpp"
 #include "row_ops.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace llm {
 
 constexpr int kLmWaves = 8;
@@ -31,11 +37,12 @@ constexpr int kLmKs = kLmKChunk / 32;
 
 struct LmHeadArgs {
   const float* x;
-  const _Float16* E;
+  const _Float16* E;  // packed: [V/16][K/32][64 lanes][8]
   float* logits;      // [M][V] (may be NULL when only the argmax is wanted)
   float* part_val;    // [M][nwg] max per (row, workgroup), or NULL
   int32_t* part_idx;  // [M][nwg]
   int M, V, K, nwg;
+  int mode;  // tuning: bit0 skip MFMA, bit1 skip x staging, bit2 skip E loads
 };
 
 // MT = 16-row tiles of x per workgroup (1, 2 or 4).
@@ -49,71 +56,100 @@ __global__ __launch_bounds__(512) void lm_head_kernel(LmHeadArgs a) {
   const int w = wave_id_uniform();
   const int m0 = blockIdx.y * 16 * MT;
   const int n0 = blockIdx.x * kLmCols + w * 16;  // this wave's 16 vocabulary rows
-  const int nrow = n0 + (lane & 15);
-  const int kg = lane >> 4;
+  const int KS = a.K / 32;
+  const int ntile = n0 >> 4;
+  const int ntiles = (a.V + 15) / 16;
   const auto ers = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.E, (short)0, (uint32_t)min((size_t)a.V * a.K * 2, (size_t)0xFFFFFFF0u), 0x00020000);
-  const uint32_t e_off = nrow < a.V ? (uint32_t)((size_t)nrow * a.K * 2) + kg * 16 : 0xFFFFFFF0u;
+      (void*)a.E, (short)0, (uint32_t)min((size_t)ntiles * KS * 1024, (size_t)0xFFFFFFF0u), 0x00020000);
+  const uint32_t e_off = ntile < ntiles ? (uint32_t)((size_t)ntile * KS * 1024) + lane * 16 : 0xFFFFFFF0u;
 
   f32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = (a.K + kLmKChunk - 1) / kLmKChunk;  // K % 32 == 0; tail k-steps load 0
-  u32x4 eb[2][kLmKs];
   auto issue = [&](u32x4 (&dst)[kLmKs], int c) {
 #pragma unroll
     for (int ks = 0; ks < kLmKs; ++ks) {
       const int k = c * kLmKChunk + ks * 32;
-      const uint32_t off = (e_off == 0xFFFFFFF0u || k >= a.K) ? 0xFFFFFFF0u : e_off + (uint32_t)k * 2;
-      dst[ks] = __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: read once, nt
+      const uint32_t off = (e_off == 0xFFFFFFF0u || k >= a.K) ? 0xFFFFFFF0u : e_off + (uint32_t)(k / 32) * 1024u;
+      dst[ks] = (a.mode & 4) ? u32x4{0u, 0u, 0u, (uint32_t)ks}
+                             : __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: read once, nt
     }
   };
   // Stage x[m0:m0+16MT][c*256 : +256] as hi/lo A fragments: fragment (mt, ks)
-  // lane l holds row mt*16 + (l&15), k = ks*32 + 8*(l>>4) .. +8.
-  auto stage_x = [&](int c) {
-    constexpr int FR = MT * kLmKs * 64;  // (mt, ks, lane) fragments of 8 values
-    for (int f = threadIdx.x; f < FR; f += 512) {
+  // lane l holds row mt*16 + (l&15), k = ks*32 + 8*(l>>4) .. +8.  Each thread
+  // owns FPT fragments; chunk c+1's x is loaded into registers while chunk c
+  // is multiplied.
+  constexpr int FPT = MT * kLmKs * 64 / 512;  // fragments per thread (1, 2 or 4)
+  f32x4 xr[FPT][2];
+  auto load_x = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < FPT; ++i) {
+      const int f = threadIdx.x + i * 512;
       const int l = f & 63, ks = (f >> 6) % kLmKs, mt = (f >> 6) / kLmKs;
       const int row = m0 + mt * 16 + (l & 15);
       const int k = c * kLmKChunk + ks * 32 + 8 * (l >> 4);
-      f32x4 v0{0.f, 0.f, 0.f, 0.f}, v1{0.f, 0.f, 0.f, 0.f};
-      if (row < a.M && k < a.K) {
+      xr[i][0] = xr[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (row < a.M && k < a.K && !(a.mode & 2)) {
         const f32x4* src = reinterpret_cast<const f32x4*>(a.x + (size_t)row * a.K + k);
-        v0 = src[0];
-        v1 = src[1];
+        xr[i][0] = src[0];
+        xr[i][1] = src[1];
       }
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int i = 0; i < FPT; ++i) {
+      const int f = threadIdx.x + i * 512;
+      const int l = f & 63, ks = (f >> 6) % kLmKs, mt = (f >> 6) / kLmKs;
       f16x8 hi, lo;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        hi[e] = (_Float16)v0[e];
-        hi[4 + e] = (_Float16)v1[e];
-        lo[e] = (_Float16)(v0[e] - (float)hi[e]);
-        lo[4 + e] = (_Float16)(v1[e] - (float)hi[4 + e]);
+        hi[e] = (_Float16)xr[i][0][e];
+        hi[4 + e] = (_Float16)xr[i][1][e];
+        lo[e] = (_Float16)(xr[i][0][e] - (float)hi[e]);
+        lo[4 + e] = (_Float16)(xr[i][1][e] - (float)hi[4 + e]);
       }
       xa[mt][ks][0][l] = __builtin_bit_cast(u32x4, hi);
       xa[mt][ks][1][l] = __builtin_bit_cast(u32x4, lo);
     }
   };
 
-  issue(eb[0], 0);
-  for (int c = 0; c < nchunks; ++c) {
-    stage_x(c);
+  // One chunk: stage x, then multiply while the next chunk's E and x loads are
+  // in flight.  The two E buffers are distinct named arrays (static register
+  // indexing: a dynamically indexed register array would live in scratch).
+  auto chunk = [&](const u32x4 (&cur)[kLmKs], u32x4 (&nxt)[kLmKs], int c) {
+    store_x();
     __syncthreads();
-    if (c + 1 < nchunks) issue(eb[(c + 1) & 1], c + 1);
-    const u32x4(&cur)[kLmKs] = eb[c & 1];
+    if (c + 1 < nchunks) {
+      issue(nxt, c + 1);
+      load_x(c + 1);
+    }
+    if (a.mode & 1) {
+      acc[0][0] += __builtin_bit_cast(float, cur[0][0] ^ cur[kLmKs - 1][3]) * 0.f +
+                   (float)xa[0][0][0][lane][0];
+    } else {
 #pragma unroll
-    for (int ks = 0; ks < kLmKs; ++ks) {
-      const f16x8 bb = __builtin_bit_cast(f16x8, cur[ks]);
+      for (int ks = 0; ks < kLmKs; ++ks) {
+        const f16x8 bb = __builtin_bit_cast(f16x8, cur[ks]);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const f16x8 hi = __builtin_bit_cast(f16x8, xa[mt][ks][0][lane]);
-        const f16x8 lo = __builtin_bit_cast(f16x8, xa[mt][ks][1][lane]);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bb, acc[mt], 0, 0, 0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bb, acc[mt], 0, 0, 0);
+        for (int mt = 0; mt < MT; ++mt) {
+          const f16x8 hi = __builtin_bit_cast(f16x8, xa[mt][ks][0][lane]);
+          const f16x8 lo = __builtin_bit_cast(f16x8, xa[mt][ks][1][lane]);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bb, acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bb, acc[mt], 0, 0, 0);
+        }
       }
     }
     __syncthreads();  // xa is rewritten by the next chunk
+  };
+  u32x4 eA[kLmKs], eB[kLmKs];
+  issue(eA, 0);
+  load_x(0);
+  for (int c = 0; c < nchunks; c += 2) {
+    chunk(eA, eB, c);
+    if (c + 1 < nchunks) chunk(eB, eA, c + 1);
   }
 
   // acc[mt] lane l, reg r: x row m0 + mt*16 + 4*(l>>4) + r, vocab row n0 + (l&15)
@@ -186,10 +222,44 @@ __global__ __launch_bounds__(256) void argmax_partials_kernel(const float* __res
 
 int lm_head_workgroups(int V) { return (V + kLmCols - 1) / kLmCols; }
 
+// E [V][K] row-major -> B-fragment order: block (vocab tile t, k-step s) is
+// 1 KiB; lane l holds E[16 t + (l & 15)][32 s + 8 (l >> 4) + j], j < 8.
+__global__ void lm_pack_kernel(const _Float16* __restrict__ E, _Float16* __restrict__ P, int V,
+                               int K) {
+  const size_t KS = K / 32;
+  const size_t total = (size_t)((V + 15) / 16) * KS * 64;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int lane = idx & 63;
+    const size_t blk = idx >> 6;
+    const int s = blk % KS;
+    const int t = blk / KS;
+    const int v = t * 16 + (lane & 15);
+    const int k = s * 32 + 8 * (lane >> 4);
+    u32x4 val{0u, 0u, 0u, 0u};
+    if (v < V) val = *reinterpret_cast<const u32x4*>(E + (size_t)v * K + k);
+    reinterpret_cast<u32x4*>(P)[idx] = val;
+  }
+}
+
+size_t lm_head_packed_bytes(int V, int K) { return (size_t)((V + 15) / 16) * (K / 32) * 1024; }
+
+hipError_t launch_lm_pack(const void* E, void* P, int V, int K, hipStream_t st) {
+  const size_t total = lm_head_packed_bytes(V, K) / 16;
+  const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(lm_pack_kernel, dim3(blocks), dim3(256), 0, st,
+                     static_cast<const _Float16*>(E), static_cast<_Float16*>(P), V, K);
+  return hipGetLastError();
+}
+
 hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, int V, int K,
                           float* part_val, int32_t* part_idx, hipStream_t st) {
+  static const int mode = [] {
+    const char* v = std::getenv("LLM_LM_MODE");
+    return v ? std::atoi(v) : 0;
+  }();
   LmHeadArgs a{x, static_cast<const _Float16*>(E), logits, part_val, part_idx, M, V, K,
-               lm_head_workgroups(V)};
+               lm_head_workgroups(V), mode};
   const int mt = M <= 16 ? 1 : M <= 32 ? 2 : 4;
   const dim3 grid(a.nwg, (M + 16 * mt - 1) / (16 * mt)), block(512);
   if (mt == 1) hipLaunchKernelGGL(lm_head_kernel<1>, grid, block, 0, st, a);
@@ -215,7 +285,14 @@ extern "C" int lm_head(const float* x, const void* E, float* logits, int M, int 
   if (M == 0) return LLM_OK;
   LLM_REQUIRE(x && E && logits, "lm_head: NULL operand");
   LLM_REQUIRE(K % 32 == 0, "lm_head: K must be a multiple of 32");
-  LLM_REQUIRE((size_t)V * K * 2 < 0xFFFFFFF0ull, "lm_head: E too large for 32-bit offsets");
-  LLM_HIP_RET(launch_lm_head(x, E, logits, M, V, K, nullptr, nullptr, as_stream(stream)));
+  LLM_REQUIRE(lm_head_packed_bytes(V, K) < 0xFFFFFFF0ull, "lm_head: E too large for 32-bit offsets");
+  // one-shot entry: pack E into a scratch copy (the decoder packs once at load)
+  hipStream_t st = as_stream(stream);
+  void* P = nullptr;
+  LLM_HIP_RET(hipMallocAsync(&P, lm_head_packed_bytes(V, K), st));
+  hipError_t e = launch_lm_pack(E, P, V, K, st);
+  if (e == hipSuccess) e = launch_lm_head(x, P, logits, M, V, K, nullptr, nullptr, st);
+  (void)hipFreeAsync(P, st);
+  if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("lm_head: ") + hipGetErrorString(e));
   return LLM_OK;
 }

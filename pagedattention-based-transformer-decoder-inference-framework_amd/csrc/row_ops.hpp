@@ -29,9 +29,11 @@ hipError_t launch_kv_append(const float* qkv, int rows, int H, int D, const int3
                             int num_pages, void* k_pool, void* v_pool, hipStream_t st);
 hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* val, int n,
                               hipStream_t st);
-// LM head (csrc/lm_head.hip): logits = x . E^T; with part_val/part_idx also the
+// LM head (csrc/lm_head.hip): logits = x . E^T (E packed by launch_lm_pack); with part_val/part_idx also the
 // per-(row, workgroup) first maxima that launch_argmax_partials reduces to ids.
 int lm_head_workgroups(int V);
+size_t lm_head_packed_bytes(int V, int K);
+hipError_t launch_lm_pack(const void* E, void* P, int V, int K, hipStream_t st);  // E -> packed
 hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, int V, int K,
                           float* part_val, int32_t* part_idx, hipStream_t st);
 hipError_t launch_argmax_partials(const float* part_val, const int32_t* part_idx, int M, int nwg,

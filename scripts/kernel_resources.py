@@ -13,11 +13,11 @@ cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fP
        "-c", src, "-o", "/tmp/_kr.o", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur = None
-short = {"VGPRs": "vgpr", "AGPRs": "agpr", "VGPRs Spill": "spill",
+short = {"VGPRs": "vgpr", "AGPRs": "agpr", "VGPRs Spill": "spill", "ScratchSize [bytes/lane]": "scratch",
          "Occupancy [waves/SIMD]": "occ", "LDS Size [bytes/block]": "lds"}
 for line in out.splitlines():
-    m = re.search(r"(?:remark: |\s)(Function Name|VGPRs|AGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]|"
-                  r"LDS Size \[bytes/block\]): (\S+)", line)
+    m = re.search(r"(?:remark: |\s)(Function Name|VGPRs|AGPRs|VGPRs Spill|ScratchSize \[bytes/lane\]|"
+                  r"Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\S+)", line)
     if not m:
         continue
     k, v = m.groups()
