@@ -89,8 +89,16 @@ constexpr int kKvLoadAux = 2;
 // STAGES = register stages in flight per wave (2: the next chunk loads while
 // the current one is computed; 1: latency hidden by occupancy alone).
 // MIN_WAVES > 0 asks the compiler for that many waves per SIMD.
+// BEAM: beam-aware KV prefetch for row_group == 4 (one workgroup = the 4
+// beams of one sequence for one (head, split)).  When the 4 rows are valid and
+// hold equal contexts, the leading chunks whose pages all 4 rows share (a
+// forked prefix) are fetched ONCE per workgroup: each wave loads a quarter of
+// the chunk, the quarters meet in LDS (double-buffered, one barrier per chunk,
+// the next chunk's quarter in flight during the current chunk's math) and
+// every wave runs its own softmax/AV over the full chunk from LDS.  The rest
+// of the split (beam-private pages) takes the per-wave direct path.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
-          int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false>
+          int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
   constexpr int LPT = D / 8;
@@ -103,13 +111,32 @@ void pa_split_kernel(PaSplitArgs a) {
 
   const int lane = lane_id();
   const int wid = blockIdx.x * 4 + wave_id_uniform();
-  const int G = a.group;
+  const int G = BEAM ? 4 : a.group;
   const int gi = wid % G;  // row within the group (fastest: adjacent waves)
   const int rest = wid / G;
   const int s = rest % a.nsplit;
   const int gh = rest / a.nsplit;
   const int h = gh % a.H;
   const int b = (gh / a.H) * G + gi;
+  // BEAM: the shared path runs only when all 4 rows exist, route to a valid
+  // page-table row and hold the same context (a uniform decision: every wave
+  // of the workgroup evaluates the same 4 rows, before any early return).
+  bool share = false;
+  if constexpr (BEAM) {
+    share = true;
+    const int g0 = b - gi;
+    int T0 = -1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int bi = g0 + i;
+      if (bi >= a.B) { share = false; break; }
+      const int ri = a.beam_ids ? a.beam_ids[bi] : bi;
+      int Ti = a.context_lens ? a.context_lens[bi] : a.T;
+      Ti = min(max(Ti, 0), a.T);
+      if (ri < 0 || ri >= a.num_beams || (i > 0 && Ti != T0)) { share = false; break; }
+      T0 = Ti;
+    }
+  }
   if (b >= a.B) return;
   const int bh = b * a.H + h;
   const size_t pidx = (size_t)bh * a.nsplit + s;  // partial-state slot
@@ -237,16 +264,88 @@ void pa_split_kernel(PaSplitArgs a) {
   };
 
   const int nchunks = (count + U - 1) / U;
+  int ch0 = 0;  // first chunk of the per-wave direct path
+  if constexpr (BEAM) {
+    static_assert(NR % 2 == 0, "beam prefetch splits a chunk's 2*NR pieces in quarters");
+    constexpr int QP = NR / 2;  // pieces per wave per chunk
+    __shared__ int pid_lds[4][128];
+    __shared__ __attribute__((aligned(16))) u32x4 kvbuf[2][2 * NR][64];
+    if (share) {
+      pid_lds[gi][lane] = pid0;
+      pid_lds[gi][64 + lane] = pid1;
+      __syncthreads();
+      const bool e0 = pid_lds[0][lane] == pid_lds[1][lane] && pid_lds[0][lane] == pid_lds[2][lane] &&
+                      pid_lds[0][lane] == pid_lds[3][lane];
+      const int l1 = 64 + lane;
+      const bool e1 = pid_lds[0][l1] == pid_lds[1][l1] && pid_lds[0][l1] == pid_lds[2][l1] &&
+                      pid_lds[0][l1] == pid_lds[3][l1];
+      const uint64_t mk0 = __ballot(e0), mk1 = __ballot(e1);
+      int nsh = 0;  // leading chunks whose pages are all shared (uniform)
+      for (; nsh < nchunks; ++nsh) {
+        bool all = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = nsh * U + u;
+          if (j < count) all = all && (((j < 64 ? mk0 >> j : mk1 >> (j - 64)) & 1ull) != 0);
+        }
+        if (!all) break;
+      }
+      nsh = __builtin_amdgcn_readfirstlane(nsh);
+      // this wave's quarter of chunk cc: pieces q = gi*QP + t of [K pieces | V pieces]
+      auto quarter = [&](u32x4 (&qr)[QP], int cc) {
+#pragma unroll
+        for (int t = 0; t < QP; ++t) {
+          const int q = gi * QP + t;
+          const int pi = q % NR;
+          const int u = pi / NI, i = pi % NI;
+          const int j = cc * U + u;
+          const int pg = page_of(min(j, kMaxPps - 1));
+          const bool ok = (j < count) && (pg >= 0);
+          const size_t off = (size_t)(ok ? pg : 0) * PAGE_BYTES;
+          const uint8_t* pool = q < NR ? a.k_pool : a.v_pool;
+          const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pool + off), (short)0,
+                                                            ok ? PAGE_BYTES : 0, 0x00020000);
+          qr[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + i * 1024, 0, AUX);
+        }
+      };
+      if (nsh > 0) {
+        u32x4 qr[QP];
+        quarter(qr, 0);
+#pragma unroll
+        for (int t = 0; t < QP; ++t) kvbuf[0][gi * QP + t][lane] = qr[t];
+        if (nsh > 1) quarter(qr, 1);
+        __syncthreads();
+        for (int cc = 0; cc < nsh; ++cc) {
+          const int cur = cc & 1;
+          u32x4 kk[NR], vv[NR];
+#pragma unroll
+          for (int p = 0; p < NR; ++p) {
+            kk[p] = kvbuf[cur][p][lane];
+            vv[p] = kvbuf[cur][NR + p][lane];
+          }
+          compute(kk, vv, cc * U);
+          if (cc + 1 < nsh) {
+            // buf[cur ^ 1] was last read in iteration cc - 1, before its barrier
+#pragma unroll
+            for (int t = 0; t < QP; ++t) kvbuf[cur ^ 1][gi * QP + t][lane] = qr[t];
+            if (cc + 2 < nsh) quarter(qr, cc + 2);
+          }
+          __syncthreads();
+        }
+      }
+      ch0 = nsh;
+    }
+  }
   if constexpr (STAGES == 1) {
     u32x4 kA[NR], vA[NR];
-    for (int ch = 0; ch < nchunks; ++ch) {
+    for (int ch = ch0; ch < nchunks; ++ch) {
       issue(kA, vA, ch * U);
       compute(kA, vA, ch * U);
     }
-  } else {
+  } else if (ch0 < nchunks) {
     u32x4 kA[NR], vA[NR], kB[NR], vB[NR];
-    issue(kA, vA, 0);
-    for (int ch = 0; ch < nchunks; ch += 2) {
+    issue(kA, vA, ch0 * U);
+    for (int ch = ch0; ch < nchunks; ch += 2) {
       issue(kB, vB, (ch + 1) * U);  // past-the-end chunks load nothing (num_records 0)
       compute(kA, vA, ch * U);
       if (ch + 1 >= nchunks) break;
@@ -464,7 +563,10 @@ template <int D, int TS>
 hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_t st) {
   const int waves = ((a.B + a.group - 1) / a.group) * a.group * a.H * a.nsplit;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (lean) {
+  if (a.group == 4 && !direct && !lean) {
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, 2, 0, false, true>), grid,
+                       block, 0, st, a);
+  } else if (lean) {
     if (direct)
       hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
     else

@@ -172,13 +172,18 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle):
     kp = (rng.standard_normal((num_pages, ts, D)) * D ** -0.25).astype(np.float16)
     vp = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
     q = (rng.standard_normal((B, H, D)) * D ** -0.25).astype(np.float32)
-    lens = rng.integers(shared * ts, T + 1, size=B).astype(np.int32)
-    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T,
-                                 context_lens=lens)
     d = lambda a: torch.from_numpy(a).cuda()
-    plain = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens)).cpu().numpy()
-    assert rel_err(plain, ref) < 1e-3
-    for g in (2, 4):
-        outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
-                                  row_group=g).cpu().numpy()
-        np.testing.assert_array_equal(outg, plain)
+    # ragged contexts (groups fall back to per-wave loads), then equal contexts per
+    # 4-beam group (the shared prefix pages go through the LDS prefetch)
+    lens_ragged = rng.integers(shared * ts, T + 1, size=B).astype(np.int32)
+    lens_equal = np.repeat(rng.integers(shared * ts, T + 1, size=seqs), W).astype(np.int32)
+    for lens in (lens_ragged, lens_equal):
+        ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T,
+                                     context_lens=lens)
+        plain = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T,
+                                   context_lens=d(lens)).cpu().numpy()
+        assert rel_err(plain, ref) < 1e-3
+        for g in (2, 4):
+            outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                                      row_group=g).cpu().numpy()
+            np.testing.assert_array_equal(outg, plain)
