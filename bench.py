@@ -54,6 +54,11 @@ CONFIGS = {
                workload="C4: beam=4 INT8 decode, 8 seqs x 4 beams (24-layer/16-head/d=128), "
                         "KV context 4096 = 3840 shared (page-table fork) + 256 per beam, "
                         "beam-aware attention schedule"),
+    # BASELINE.json configs[4], per GPU: 64 of the 512 rows on each of 8 GPUs
+    # (KV 275 GB per GPU at context 8192: the page pool fills the card)
+    "c5": dict(cls="INT8Decoder", L=32, H=32, D=128, V=50257, B=64, T=8192, ts=16,
+               workload="C5 (per GPU): INT8 decoder, 32-layer/32-head/d=128, 64 seqs/GPU "
+                        "(512 over 8 GPUs), KV context 8192, page 16"),
     # BASELINE.json configs[1]
     "c2": dict(cls="CUDADecoder", L=12, H=12, D=64, V=50257, B=16, T=2048, ts=16,
                workload="C2: fp16 paged decode, 12-layer/12-head/d=64, 16 seqs/GPU, "
