@@ -31,7 +31,10 @@ enum llm_status {
   LLM_ERR_IO = 5            /* weight / cache file I/O */
 };
 
-enum llm_dtype { LLM_F16 = 0, LLM_I8 = 1, LLM_F32 = 2 };
+/* Element types.  KV pools may be any of the four (the T of
+ * AttentionCUDA::forward, attention/attention_cuda.cu:58-94: __half, bf16,
+ * int8_t (raw values, no scale), float); weights are LLM_I8 or LLM_F16. */
+enum llm_dtype { LLM_F16 = 0, LLM_I8 = 1, LLM_F32 = 2, LLM_BF16 = 3 };
 enum llm_act { LLM_ACT_NONE = 0, LLM_ACT_RELU = 1, LLM_ACT_GELU = 2 };
 
 const char* llm_last_error(void);
@@ -50,7 +53,7 @@ int llm_abi_version(void);
  * page_table[(beam*num_heads + head)*max_tiles + tile]; a page < 0 or
  * >= num_pages means "no tile" (its tokens are masked). */
 typedef struct pa_kv_view {
-  const void* k_pool;         /* [num_pages][page_size][head_dim] fp16 */
+  const void* k_pool;         /* [num_pages][page_size][head_dim] of kv_dtype */
   const void* v_pool;         /* same layout */
   const int32_t* page_table;  /* [num_beams][num_heads][max_tiles] int32, device */
   int32_t num_pages;
@@ -59,7 +62,8 @@ typedef struct pa_kv_view {
   int32_t num_beams;
   int32_t num_heads;
   int32_t max_tiles;
-  int32_t kv_dtype;           /* LLM_F16 */
+  int32_t kv_dtype;           /* LLM_F16 (default), LLM_BF16, LLM_F32 or LLM_I8; one page
+                               * (page_size * head_dim elements) must be 1..16 KiB */
 } pa_kv_view;
 
 /* Bytes of device workspace pa_decode needs (split-T partial softmax state). */
@@ -168,6 +172,11 @@ typedef struct kv_cache kv_cache;
 
 int kv_cache_create(int num_layers, int num_beams, int num_heads, int head_dim, int page_size,
                     int max_tiles, long long num_pages, kv_cache** out);
+/* kv_cache_create with pools of kv_dtype elements (KVTileCache<T>,
+ * kv_cache/kv_tile_cache.hpp:9 with T in {__half, bf16, int8_t, float}). */
+int kv_cache_create_typed(int num_layers, int num_beams, int num_heads, int head_dim,
+                          int page_size, int max_tiles, long long num_pages, int kv_dtype,
+                          kv_cache** out);
 void kv_cache_destroy(kv_cache* c);
 int kv_cache_view(const kv_cache* c, int layer, pa_kv_view* out);
 long long kv_cache_num_pages(const kv_cache* c);
@@ -190,8 +199,8 @@ int kv_cache_release(kv_cache* c, int beam);
 int kv_cache_clear(kv_cache* c);
 /* PageTable::sync_to_gpu (page_table.cpp:59-62): push dirty host entries. */
 int kv_cache_sync(kv_cache* c, void* stream);
-/* Copy n tokens of fp16 K and V (host, [n][H][D]) for `beam` starting at token
- * position pos into the pools of `layer` (pages must be reserved). */
+/* Copy n tokens of K and V (host, [n][H][D] in the cache's kv_dtype) for
+ * `beam` starting at token position pos into the pools of `layer`. */
 int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, int n, const void* k_host,
                           const void* v_host);
 /* Device pointers of the pools / table (for tests and custom kernels). */

@@ -242,26 +242,34 @@ class KVTileCache {
  public:
   KVTileCache() = default;
   ~KVTileCache() { if (c_) kv_cache_destroy(c_); }
+  // dtype: the T of KVTileCache<T> — "float16" (default), "bfloat16", "float32", "int8"
   void init(int num_pages, int tile_size, int head_dim, int num_layers, int num_beams,
-            int num_heads, int max_tiles) {
+            int num_heads, int max_tiles, const std::string& dtype) {
+    const int kvt = dtype == "float16" || dtype == "half" ? LLM_F16
+                    : dtype == "bfloat16"                 ? LLM_BF16
+                    : dtype == "float32" || dtype == "float" ? LLM_F32
+                    : dtype == "int8"                     ? LLM_I8
+                                                          : -1;
+    if (kvt < 0) throw std::invalid_argument("KVTileCache: dtype must be float16, bfloat16, float32 or int8");
     if (c_) { kv_cache_destroy(c_); c_ = nullptr; }
-    check(kv_cache_create(num_layers, num_beams, num_heads, head_dim, tile_size, max_tiles,
-                          num_pages, &c_));
+    check(kv_cache_create_typed(num_layers, num_beams, num_heads, head_dim, tile_size, max_tiles,
+                                num_pages, kvt, &c_));
     tile_size_ = tile_size; head_dim_ = head_dim; layers_ = num_layers; beams_ = num_beams;
-    heads_ = num_heads; max_tiles_ = max_tiles;
+    heads_ = num_heads; max_tiles_ = max_tiles; dtype_ = dtype;
+    es_ = kvt == LLM_F32 ? 4 : kvt == LLM_I8 ? 1 : 2;
   }
   void resize(int new_num_pages, int new_tile_size) {  // kv_tile_cache.cpp:26-37: drops contents
-    init(new_num_pages, new_tile_size, head_dim_, layers_, beams_, heads_, max_tiles_);
+    init(new_num_pages, new_tile_size, head_dim_, layers_, beams_, heads_, max_tiles_, dtype_);
   }
   uintptr_t get_key_ptr(int page) const {
     need();
     if (page < 0 || page >= kv_cache_num_pages(c_)) throw std::out_of_range("page id");
-    return reinterpret_cast<uintptr_t>(kv_cache_k_pool(c_)) + (uintptr_t)page * tile_size_ * head_dim_ * 2;
+    return reinterpret_cast<uintptr_t>(kv_cache_k_pool(c_)) + (uintptr_t)page * tile_size_ * head_dim_ * es_;
   }
   uintptr_t get_value_ptr(int page) const {
     need();
     if (page < 0 || page >= kv_cache_num_pages(c_)) throw std::out_of_range("page id");
-    return reinterpret_cast<uintptr_t>(kv_cache_v_pool(c_)) + (uintptr_t)page * tile_size_ * head_dim_ * 2;
+    return reinterpret_cast<uintptr_t>(kv_cache_v_pool(c_)) + (uintptr_t)page * tile_size_ * head_dim_ * es_;
   }
   int register_tile(int beam, int head, int tile, int layer) {
     need();
@@ -278,11 +286,15 @@ class KVTileCache {
   void sync_page_table_to_gpu() { need(); check(kv_cache_sync(c_, nullptr)); check(llm_sync()); }
   void save_to_file(const std::string& p) { need(); check(kv_cache_save(c_, p.c_str())); }
   void load_from_file(const std::string& p) { need(); check(kv_cache_load(c_, p.c_str())); }
-  void write_tokens(int layer, int beam, int pos, py::array_t<uint16_t, py::array::c_style | py::array::forcecast> k,
-                    py::array_t<uint16_t, py::array::c_style | py::array::forcecast> v) {
+  // k / v: C-contiguous [n][H][D] arrays whose items are the cache's element
+  // bits (fp16/bf16 as uint16 or float16, float32, int8).
+  void write_tokens(int layer, int beam, int pos, py::array k, py::array v) {
     need();
-    if (k.size() != v.size() || k.size() % ((size_t)heads_ * head_dim_) != 0)
-      throw std::invalid_argument("write_tokens: k/v must be [n][H][D] fp16 bits");
+    const bool contig = (k.flags() & py::array::c_style) && (v.flags() & py::array::c_style);
+    if (!contig || k.itemsize() != es_ || v.itemsize() != es_ || k.size() != v.size() ||
+        k.size() % ((size_t)heads_ * head_dim_) != 0)
+      throw std::invalid_argument("write_tokens: k/v must be C-contiguous [n][H][D] arrays of the "
+                                  "cache's element size");
     const int n = (int)(k.size() / ((size_t)heads_ * head_dim_));
     check(kv_cache_write_tokens(c_, layer, beam, pos, n, k.data(), v.data()));
   }
@@ -296,6 +308,7 @@ class KVTileCache {
     d["page_table"] = reinterpret_cast<uintptr_t>(v.page_table);
     d["num_pages"] = v.num_pages; d["page_size"] = v.page_size; d["head_dim"] = v.head_dim;
     d["num_beams"] = v.num_beams; d["num_heads"] = v.num_heads; d["max_tiles"] = v.max_tiles;
+    d["kv_dtype"] = v.kv_dtype;
     return d;
   }
   long long free_pages() const { need(); return kv_cache_free_pages(c_); }
@@ -307,6 +320,8 @@ class KVTileCache {
   void need() const { if (!c_) throw std::runtime_error("KVTileCache: call init() first"); }
   kv_cache* c_ = nullptr;
   int tile_size_ = 0, head_dim_ = 0, layers_ = 1, beams_ = 1, heads_ = 1, max_tiles_ = 1;
+  int es_ = 2;
+  std::string dtype_ = "float16";
 };
 
 // PageTable (kv_cache/page_table.hpp:5-37): a one-layer table whose entries
@@ -390,7 +405,7 @@ PYBIND11_MODULE(llm_decoder, m) {
       .def(py::init<>())
       .def("init", &KVTileCache::init, py::arg("num_pages"), py::arg("tile_size"),
            py::arg("head_dim"), py::arg("num_layers") = 1, py::arg("num_beams") = 1,
-           py::arg("num_heads") = 1, py::arg("max_tiles") = 1)
+           py::arg("num_heads") = 1, py::arg("max_tiles") = 1, py::arg("dtype") = "float16")
       .def("resize", &KVTileCache::resize)
       .def("get_key_ptr", &KVTileCache::get_key_ptr)
       .def("get_value_ptr", &KVTileCache::get_value_ptr)

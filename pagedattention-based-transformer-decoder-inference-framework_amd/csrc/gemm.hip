@@ -186,10 +186,51 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     }
   };
 
+  // Epilogue operands are independent of the accumulators: load them before
+  // the k loop so their round trips (scales, bias, and for KV append the
+  // dependent pos -> page-table chain) overlap the weight stream instead of
+  // following it.  Thread t owns outputs t, t + NTHR, ... (col fastest).
+  constexpr int ROWS = 16 * MT, COLS = 16 * NT, NTHR = WAVES * 64;
+  constexpr int EPT = (ROWS * COLS + NTHR - 1) / NTHR;
+  const KvAppend& kv = a.kv;
+  const int hid = kv.H * kv.D;
+  float e_scale[EPT], e_bias[EPT];
+  int e_pos[EPT], e_br[EPT], e_page[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int o = threadIdx.x + e * NTHR;
+    const int m = m0 + o / COLS;
+    const int n = nt0 * 16 + o % COLS;
+    const bool valid = o < ROWS * COLS && m < a.M && n < a.N;
+    e_scale[e] = 1.f;
+    if constexpr (KIND == GemmKind::I8) {
+      if (valid && a.sa) e_scale[e] *= a.sa[m];
+      if (valid && a.sw) e_scale[e] *= a.sw[n];
+    }
+    e_bias[e] = valid && a.bias ? a.bias[n] : 0.f;
+    const bool kvcol = valid && kv.k_pool && n >= hid;
+    e_pos[e] = kvcol ? kv.pos[m] : -1;
+    e_br[e] = kvcol ? (kv.rows ? kv.rows[m] : m) : -1;
+  }
+
   {
     Batch b0, b1;
     int ks = ks0;
     if (ks < ks1) issue(b0, ks);
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int o = threadIdx.x + e * NTHR;
+      const int n = nt0 * 16 + o % COLS;
+      const int p = e_pos[e], br = e_br[e];
+      int page = -1;
+      if (p >= 0 && br >= 0 && br < kv.num_beams && p / kv.TS < kv.max_tiles) {
+        const int which = n >= 2 * hid;
+        const int h = (n - hid * (1 + which)) / kv.D;
+        page = kv.page_table[((size_t)br * kv.H + h) * kv.max_tiles + p / kv.TS];
+        if (page >= kv.num_pages) page = -1;
+      }
+      e_page[e] = page;
+    }
     while (ks < ks1) {
       if (ks + kUnroll < ks1) issue(b1, ks + kUnroll);
       compute(b0);
@@ -207,10 +248,11 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     for (int j = 0; j < NT; ++j) red[w][mt * NT + j][lane] = acc[mt][j];
   __syncthreads();
 
-  // Epilogue: thread t -> (row, col) with col fastest (64-byte row segments).
-  constexpr int ROWS = 16 * MT, COLS = 16 * NT;
-
-  for (int o = threadIdx.x; o < ROWS * COLS; o += WAVES * 64) {
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+#pragma clang fp contract(off)  // y = acc * scale + bias rounded twice, as the reference
+    const int o = threadIdx.x + e * NTHR;
+    if (o >= ROWS * COLS) break;
     const int cl = o % COLS;
     const int row = o / COLS;
     const int j = cl >> 4;
@@ -228,36 +270,23 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][src_lane][reg];
       if (a.acc_out) a.acc_out[(size_t)m * a.N + n] = s;
-      if (!a.C && !a.kv.k_pool) continue;
-      const float scale = (a.sa ? a.sa[m] : 1.f) * (a.sw ? a.sw[n] : 1.f);
-      y = __fmul_rn((float)s, scale);
-      if (a.bias) y = __fadd_rn(y, a.bias[n]);
+      y = (float)s * e_scale[e];
+      if (a.bias) y = y + e_bias[e];
     } else {
       float s = 0.f;
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][src_lane][reg];
-      y = a.bias ? s + a.bias[n] : s;
+      y = a.bias ? s + e_bias[e] : s;
     }
     y = apply_act(y, a.act);
     if (a.C && n < a.c_cols) a.C[(size_t)m * a.c_ld + n] = y;
-    {
-      const KvAppend& kv = a.kv;
-      const int hid = kv.H * kv.D;
-      const int br = kv.rows ? kv.rows[m] : m;
-      if (kv.k_pool && n >= hid && br >= 0 && br < kv.num_beams) {
-        const int which = n >= 2 * hid;  // 0: K, 1: V
-        const int i = n - hid * (1 + which);
-        const int h = i / kv.D, d = i - h * kv.D;
-        const int p = kv.pos[m];
-        const int tile = p / kv.TS;
-        if (tile < kv.max_tiles) {
-          const int page = kv.page_table[((size_t)br * kv.H + h) * kv.max_tiles + tile];
-          if (page >= 0 && page < kv.num_pages) {
-            const size_t off = ((size_t)page * kv.TS + (p - tile * kv.TS)) * kv.D + d;
-            (which ? kv.v_pool : kv.k_pool)[off] = (_Float16)y;
-          }
-        }
-      }
+    if (e_page[e] >= 0) {
+      const int which = n >= 2 * hid;  // 0: K, 1: V
+      const int i = n - hid * (1 + which);
+      const int d = i % kv.D;
+      const int p = e_pos[e];
+      const size_t off = ((size_t)e_page[e] * kv.TS + (p % kv.TS)) * kv.D + d;
+      (which ? kv.v_pool : kv.k_pool)[off] = (_Float16)y;
     }
   }
 }

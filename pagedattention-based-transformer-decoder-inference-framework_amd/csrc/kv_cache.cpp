@@ -29,12 +29,13 @@
 
 namespace llm {
 
-// src [n][H][D] fp16 rows for token positions pos0..pos0+n-1 of `beam`.
-__global__ void kv_write_tokens_kernel(const _Float16* __restrict__ ksrc,
-                                       const _Float16* __restrict__ vsrc, int n, int H, int D,
-                                       int pos0, int beam, const int32_t* __restrict__ table,
-                                       int max_tiles, int TS, long long num_pages,
-                                       _Float16* __restrict__ kp, _Float16* __restrict__ vp) {
+// src [n][H][D] rows (element type E) for token positions pos0..pos0+n-1 of `beam`.
+template <typename E>
+__global__ void kv_write_tokens_kernel(const E* __restrict__ ksrc, const E* __restrict__ vsrc,
+                                       int n, int H, int D, int pos0, int beam,
+                                       const int32_t* __restrict__ table, int max_tiles, int TS,
+                                       long long num_pages, E* __restrict__ kp,
+                                       E* __restrict__ vp) {
   const size_t total = (size_t)n * H * D;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -52,10 +53,13 @@ __global__ void kv_write_tokens_kernel(const _Float16* __restrict__ ksrc,
   }
 }
 
-int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, long long pages) {
+int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, long long pages,
+                  int dtype_) {
   L = L_; beams = beams_; H = H_; D = D_; TS = TS_; max_tiles = max_tiles_; num_pages = pages;
+  dtype = dtype_;
+  es = dtype == LLM_F32 ? 4 : dtype == LLM_I8 ? 1 : 2;
   page_elems = (size_t)TS * D;
-  const size_t pool_bytes = (size_t)num_pages * page_elems * 2;
+  const size_t pool_bytes = (size_t)num_pages * page_bytes();
   if (hipMalloc(&k_pool, pool_bytes) != hipSuccess || hipMalloc(&v_pool, pool_bytes) != hipSuccess) {
     (void)hipGetLastError();
     return fail(LLM_ERR_OOM, "kv_cache: cannot allocate " + std::to_string(2 * pool_bytes) +
@@ -180,7 +184,7 @@ int KvCache::prepare_append(int beam, int pos) {
 int KvCache::sync(hipStream_t st) {
   // pending copy-on-write page copies first (old page -> new page, K and V)
   for (const auto& c : cow) {
-    const size_t bytes = page_elems * 2;
+    const size_t bytes = page_bytes();
     LLM_HIP_RET(hipMemcpyAsync((char*)k_pool + (size_t)c.second * bytes,
                                (char*)k_pool + (size_t)c.first * bytes, bytes,
                                hipMemcpyDeviceToDevice, st));
@@ -233,13 +237,24 @@ struct kv_cache {
 
 extern "C" int kv_cache_create(int num_layers, int num_beams, int num_heads, int head_dim,
                                int page_size, int max_tiles, long long num_pages, kv_cache** out) {
+  return kv_cache_create_typed(num_layers, num_beams, num_heads, head_dim, page_size, max_tiles,
+                               num_pages, LLM_F16, out);
+}
+
+extern "C" int kv_cache_create_typed(int num_layers, int num_beams, int num_heads, int head_dim,
+                                     int page_size, int max_tiles, long long num_pages,
+                                     int kv_dtype, kv_cache** out) {
   LLM_REQUIRE(out != nullptr, "kv_cache_create: out is NULL");
+  LLM_REQUIRE(kv_dtype == LLM_F16 || kv_dtype == LLM_BF16 || kv_dtype == LLM_F32 ||
+                  kv_dtype == LLM_I8,
+              "kv_cache_create: kv_dtype must be LLM_F16, LLM_BF16, LLM_F32 or LLM_I8");
   LLM_REQUIRE(num_layers > 0 && num_beams > 0 && num_heads > 0 && head_dim > 0 && page_size > 0 &&
                   max_tiles > 0 && num_pages > 0,
               "kv_cache_create: all sizes must be positive");
   LLM_REQUIRE(num_pages < (1LL << 31), "kv_cache_create: num_pages must fit int32");
   auto* c = new kv_cache();
-  int rc = c->impl.init(num_layers, num_beams, num_heads, head_dim, page_size, max_tiles, num_pages);
+  int rc = c->impl.init(num_layers, num_beams, num_heads, head_dim, page_size, max_tiles, num_pages,
+                        kv_dtype);
   if (rc) {
     delete c;
     return rc;
@@ -265,7 +280,7 @@ extern "C" int kv_cache_view(const kv_cache* c, int layer, pa_kv_view* out) {
   out->num_beams = k.beams;
   out->num_heads = k.H;
   out->max_tiles = k.max_tiles;
-  out->kv_dtype = LLM_F16;
+  out->kv_dtype = k.dtype;
   return LLM_OK;
 }
 
@@ -413,18 +428,25 @@ extern "C" int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, 
     }
   int rc = k.sync(nullptr);
   if (rc) return rc;
-  const size_t bytes = (size_t)n * k.H * k.D * 2;
+  const size_t bytes = (size_t)n * k.H * k.D * k.es;
   void *dk = nullptr, *dv = nullptr;
   LLM_HIP_RET(hipMalloc(&dk, bytes));
   LLM_HIP_RET(hipMalloc(&dv, bytes));
   LLM_HIP_RET(hipMemcpy(dk, k_host, bytes, hipMemcpyHostToDevice));
   LLM_HIP_RET(hipMemcpy(dv, v_host, bytes, hipMemcpyHostToDevice));
   const size_t total = (size_t)n * k.H * k.D;
-  hipLaunchKernelGGL(kv_write_tokens_kernel, dim3((unsigned)std::min<size_t>((total + 255) / 256, 65536)),
-                     dim3(256), 0, nullptr, static_cast<const _Float16*>(dk),
-                     static_cast<const _Float16*>(dv), n, k.H, k.D, pos, beam,
-                     k.d_table + (size_t)layer * k.beams * k.H * k.max_tiles, k.max_tiles, k.TS,
-                     k.num_pages, static_cast<_Float16*>(k.k_pool), static_cast<_Float16*>(k.v_pool));
+  const dim3 grid((unsigned)std::min<size_t>((total + 255) / 256, 65536));
+  const int32_t* table = k.d_table + (size_t)layer * k.beams * k.H * k.max_tiles;
+  auto launch = [&](auto tag) {
+    using E = decltype(tag);
+    hipLaunchKernelGGL(kv_write_tokens_kernel<E>, grid, dim3(256), 0, nullptr,
+                       static_cast<const E*>(dk), static_cast<const E*>(dv), n, k.H, k.D, pos,
+                       beam, table, k.max_tiles, k.TS, k.num_pages, static_cast<E*>(k.k_pool),
+                       static_cast<E*>(k.v_pool));
+  };
+  if (k.es == 4) launch(uint32_t{});
+  else if (k.es == 1) launch(uint8_t{});
+  else launch(uint16_t{});
   LLM_HIP_RET(hipGetLastError());
   LLM_HIP_RET(hipDeviceSynchronize());
   LLM_HIP_RET(hipFree(dk));
@@ -441,7 +463,8 @@ extern "C" int32_t* kv_cache_page_table(kv_cache* c, int layer) {
 }
 
 namespace {
-constexpr uint64_t kMagic = 0x31564B4D49505041ull;  // "APPIMKV1"
+constexpr uint64_t kMagic = 0x31564B4D49505041ull;    // "APPIMKV1": fp16 pools, 8-word header
+constexpr uint64_t kMagicV2 = 0x32564B4D49505041ull;  // "APPIMKV2": + kv_dtype word
 }
 
 extern "C" int kv_cache_save(const kv_cache* c, const char* path) {
@@ -450,7 +473,8 @@ extern "C" int kv_cache_save(const kv_cache* c, const char* path) {
   std::lock_guard<std::mutex> g(k.mu);
   std::ofstream f(path, std::ios::binary);
   if (!f) return fail(LLM_ERR_IO, std::string("kv_cache_save: cannot open ") + path);
-  const int64_t hdr[8] = {(int64_t)kMagic, k.L, k.beams, k.H, k.D, k.TS, k.max_tiles, k.num_pages};
+  const int64_t hdr[9] = {(int64_t)kMagicV2, k.L, k.beams, k.H, k.D, k.TS, k.max_tiles, k.num_pages,
+                          k.dtype};
   f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
   f.write(reinterpret_cast<const char*>(k.h_table.data()), k.entries * sizeof(int32_t));
   std::vector<int32_t> used;
@@ -459,7 +483,7 @@ extern "C" int kv_cache_save(const kv_cache* c, const char* path) {
   const int64_t nu = (int64_t)used.size();
   f.write(reinterpret_cast<const char*>(&nu), sizeof(nu));
   f.write(reinterpret_cast<const char*>(used.data()), used.size() * sizeof(int32_t));
-  const size_t pb = k.page_elems * 2;
+  const size_t pb = k.page_bytes();
   std::vector<char> buf(pb);
   LLM_HIP_RET(hipDeviceSynchronize());
   for (int32_t p : used) {
@@ -477,12 +501,18 @@ extern "C" int kv_cache_load(kv_cache* c, const char* path) {
   KvCache& k = c->impl;
   std::ifstream f(path, std::ios::binary);
   if (!f) return fail(LLM_ERR_IO, std::string("kv_cache_load: cannot open ") + path);
-  int64_t hdr[8];
-  f.read(reinterpret_cast<char*>(hdr), sizeof(hdr));
-  if (!f || hdr[0] != (int64_t)kMagic) return fail(LLM_ERR_IO, "kv_cache_load: bad header");
+  int64_t hdr[9];
+  f.read(reinterpret_cast<char*>(hdr), 8 * sizeof(int64_t));
+  if (!f || (hdr[0] != (int64_t)kMagic && hdr[0] != (int64_t)kMagicV2))
+    return fail(LLM_ERR_IO, "kv_cache_load: bad header");
+  hdr[8] = LLM_F16;
+  if (hdr[0] == (int64_t)kMagicV2) f.read(reinterpret_cast<char*>(&hdr[8]), sizeof(int64_t));
+  if (!f) return fail(LLM_ERR_IO, "kv_cache_load: bad header");
   if (hdr[1] != k.L || hdr[2] != k.beams || hdr[3] != k.H || hdr[4] != k.D || hdr[5] != k.TS ||
       hdr[6] != k.max_tiles || hdr[7] != k.num_pages)
     return fail(LLM_ERR_INVALID, "kv_cache_load: file geometry differs from this cache");
+  if (hdr[8] != k.dtype)
+    return fail(LLM_ERR_INVALID, "kv_cache_load: file kv_dtype differs from this cache");
   int rc = kv_cache_clear(c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(k.mu);
@@ -492,7 +522,7 @@ extern "C" int kv_cache_load(kv_cache* c, const char* path) {
   if (!f || nu < 0 || nu > k.num_pages) return fail(LLM_ERR_IO, "kv_cache_load: truncated");
   std::vector<int32_t> used((size_t)nu);
   f.read(reinterpret_cast<char*>(used.data()), used.size() * sizeof(int32_t));
-  const size_t pb = k.page_elems * 2;
+  const size_t pb = k.page_bytes();
   std::vector<char> buf(pb);
   for (int32_t p : used) {
     f.read(buf.data(), pb);

@@ -16,6 +16,8 @@ namespace llm {
 struct KvCache {
   int L = 0, beams = 0, H = 0, D = 0, TS = 0, max_tiles = 0;
   long long num_pages = 0;
+  int dtype = LLM_F16;  // pool element type
+  int es = 2;           // bytes per element
   size_t page_elems = 0;
   size_t entries = 0;
   void* k_pool = nullptr;
@@ -42,7 +44,9 @@ struct KvCache {
   std::mutex mu;
 
   ~KvCache();
-  int init(int L, int beams, int H, int D, int TS, int max_tiles, long long pages);
+  int init(int L, int beams, int H, int D, int TS, int max_tiles, long long pages,
+           int dtype = LLM_F16);
+  size_t page_bytes() const { return page_elems * es; }
   size_t index(int layer, int beam, int head, int tile) const {
     return (((size_t)layer * beams + beam) * H + head) * max_tiles + tile;
   }

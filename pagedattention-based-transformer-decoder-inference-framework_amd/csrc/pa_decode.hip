@@ -75,9 +75,38 @@ __device__ __forceinline__ int row_pps(int pps_fixed, int nsplit, int ntiles) {
 }
 
 // Pages per register stage: CHUNK_BYTES of K+V in flight per wave per stage.
-template <int D, int TS, int CHUNK_BYTES>
+template <int PAGE_BYTES, int CHUNK_BYTES>
 constexpr int pages_per_stage() {
-  return (CHUNK_BYTES / (2 * TS * D * 2)) > 0 ? CHUNK_BYTES / (2 * TS * D * 2) : 1;
+  return (CHUNK_BYTES / (2 * PAGE_BYTES)) > 0 ? CHUNK_BYTES / (2 * PAGE_BYTES) : 1;
+}
+
+// KV element types of the pools (AttentionCUDA::forward's T in {__half, bf16,
+// int8_t, float}, attention/attention_cuda.cu:58-94).  int8 is the raw value
+// (KVTileCache<int8_t> stores and the kernel reads it as a number, no scale).
+template <int KVT>
+constexpr int kv_elem_bytes() {
+  return KVT == LLM_F32 ? 4 : KVT == LLM_I8 ? 1 : 2;
+}
+
+// Element e of a lane's 16-byte KV piece as fp32.
+template <int KVT>
+__device__ __forceinline__ float kv_at(const u32x4& r, int e) {
+  if constexpr (KVT == LLM_F16) {
+    return (float)__builtin_bit_cast(f16x8, r)[e];
+  } else if constexpr (KVT == LLM_BF16) {
+    const uint32_t w = r[e >> 1];
+    return __uint_as_float((e & 1) ? (w & 0xFFFF0000u) : (w << 16));
+  } else if constexpr (KVT == LLM_F32) {
+    return __uint_as_float(r[e]);
+  } else {
+    return (float)(((int32_t)r[e >> 2] << (24 - 8 * (e & 3))) >> 24);
+  }
+}
+
+// A page must fill at least one wave-wide load (64 lanes x 16 B) and at most
+// one 16 KiB register stage.
+constexpr bool kv_shape_ok(int D, int TS, int es) {
+  return TS * D * es >= 1024 && TS * D * es <= 16384;
 }
 
 // KV pages are read exactly once per step: stream them with the non-temporal
@@ -98,14 +127,17 @@ constexpr int kKvLoadAux = 2;
 // every wave runs its own softmax/AV over the full chunk from LDS.  The rest
 // of the split (beam-private pages) takes the per-wave direct path.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
-          int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false>
+          int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
+          int KVT = LLM_F16>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
-  constexpr int LPT = D / 8;
+  constexpr int ES = kv_elem_bytes<KVT>();
+  constexpr int EPL = 16 / ES;  // elements per lane per 16-byte load
+  constexpr int LPT = D / EPL;
   constexpr int TPI = 64 / LPT;
   constexpr int NI = TS / TPI;
-  constexpr int PAGE_BYTES = TS * D * 2;
-  constexpr int U = pages_per_stage<D, TS, CHUNK_BYTES>();
+  constexpr int PAGE_BYTES = TS * D * ES;
+  constexpr int U = pages_per_stage<PAGE_BYTES, CHUNK_BYTES>();
   constexpr int NR = U * NI;
   static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1, "bad D/TS");
 
@@ -153,9 +185,9 @@ void pa_split_kernel(PaSplitArgs a) {
   if (count <= 0) {
     if constexpr (DIRECT) {
       if (lane < LPT) {
-        float* o = a.out + (size_t)bh * D + c * 8;
-        *reinterpret_cast<f32x4*>(o) = f32x4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f32x4*>(o + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+        float* o = a.out + (size_t)bh * D + c * EPL;
+#pragma unroll
+        for (int e = 0; e < EPL; e += 4) *reinterpret_cast<f32x4*>(o + e) = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
     return;
@@ -175,23 +207,22 @@ void pa_split_kernel(PaSplitArgs a) {
     return j < 64 ? __builtin_amdgcn_readlane(pid0, j) : __builtin_amdgcn_readlane(pid1, min(j - 64, 63));
   };
 
-  // q chunk of this lane (dims c*8 .. c*8+7), pre-scaled into log2 units.
-  float qv[8];
+  // q chunk of this lane (dims c*EPL .. c*EPL+EPL-1), pre-scaled into log2 units.
+  float qv[EPL];
   {
-    const float* qp = a.q + (size_t)b * a.q_stride + (size_t)h * D + c * 8;
-    const f32x4 q0 = *reinterpret_cast<const f32x4*>(qp);
-    const f32x4 q1 = *reinterpret_cast<const f32x4*>(qp + 4);
+    const float* qp = a.q + (size_t)b * a.q_stride + (size_t)h * D + c * EPL;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      qv[e] = q0[e] * a.qscale;
-      qv[4 + e] = q1[e] * a.qscale;
+    for (int e0 = 0; e0 < EPL; e0 += 4) {
+      const f32x4 qq = *reinterpret_cast<const f32x4*>(qp + e0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qv[e0 + e] = qq[e] * a.qscale;
     }
   }
 
   float m = kNegSentinel, l = 0.f;
-  float acc[8];
+  float acc[EPL];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
 
   const uint32_t lane_off = (uint32_t)lane * 16u;
 
@@ -234,10 +265,9 @@ void pa_split_kernel(PaSplitArgs a) {
       float mloc = kNegSentinel;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const f16x8 kh = __builtin_bit_cast(f16x8, kk[u * NI + i]);
         float d = 0.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d = fmaf(qv[e], (float)kh[e], d);
+        for (int e = 0; e < EPL; ++e) d = fmaf(qv[e], kv_at<KVT>(kk[u * NI + i], e), d);
         d = group_sum<LPT>(d);
         valid[i] = ok && (tok_base + i * TPI) < Tb;
         sc[i] = valid[i] ? d : kNegSentinel;
@@ -247,7 +277,7 @@ void pa_split_kernel(PaSplitArgs a) {
       const float corr = __builtin_amdgcn_exp2f(m - mnew);
       l *= corr;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] *= corr;
+      for (int e = 0; e < EPL; ++e) acc[e] *= corr;
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const float p = valid[i] ? __builtin_amdgcn_exp2f(sc[i] - mnew) : 0.f;
@@ -255,9 +285,8 @@ void pa_split_kernel(PaSplitArgs a) {
         // Rows past the context (or of a missing page) may hold stale bits, even
         // NaN/Inf in a never-written page: select them away (0 * NaN = NaN).
         const u32x4 vraw = valid[i] ? vv[u * NI + i] : u32x4{0u, 0u, 0u, 0u};
-        const f16x8 vh = __builtin_bit_cast(f16x8, vraw);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = fmaf(p, (float)vh[e], acc[e]);
+        for (int e = 0; e < EPL; ++e) acc[e] = fmaf(p, kv_at<KVT>(vraw, e), acc[e]);
       }
       m = mnew;
     }
@@ -364,7 +393,7 @@ void pa_split_kernel(PaSplitArgs a) {
     const float cb = __builtin_amdgcn_exp2f(mo - mn);
     l = l * ca + lo * cb;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < EPL; ++e) {
       const float ao = __shfl_xor(acc[e], off, 64);
       acc[e] = acc[e] * ca + ao * cb;
     }
@@ -374,14 +403,16 @@ void pa_split_kernel(PaSplitArgs a) {
   if (lane < LPT) {
     if constexpr (DIRECT) {
       const float inv = 1.0f / (l + 1e-6f);
-      float* o = a.out + (size_t)bh * D + c * 8;
-      *reinterpret_cast<f32x4*>(o) = f32x4{acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv};
-      *reinterpret_cast<f32x4*>(o + 4) =
-          f32x4{acc[4] * inv, acc[5] * inv, acc[6] * inv, acc[7] * inv};
+      float* o = a.out + (size_t)bh * D + c * EPL;
+#pragma unroll
+      for (int e = 0; e < EPL; e += 4)
+        *reinterpret_cast<f32x4*>(o + e) =
+            f32x4{acc[e] * inv, acc[e + 1] * inv, acc[e + 2] * inv, acc[e + 3] * inv};
     } else {
-      float* o = a.part_acc + pidx * D + c * 8;
-      *reinterpret_cast<f32x4*>(o) = f32x4{acc[0], acc[1], acc[2], acc[3]};
-      *reinterpret_cast<f32x4*>(o + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+      float* o = a.part_acc + pidx * D + c * EPL;
+#pragma unroll
+      for (int e = 0; e < EPL; e += 4)
+        *reinterpret_cast<f32x4*>(o + e) = f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
       if (lane == 0) {
         a.part_ml[pidx * 2] = m;
         a.part_ml[pidx * 2 + 1] = l;
@@ -537,15 +568,24 @@ constexpr int kMaxWavesPerCu = 32;  // 8 per SIMD x 4 SIMDs (gfx950)
 
 // Resident waves of the whole chip for one split-kernel instantiation
 // (occupancy query x CU count), cached.  Fallback: 256 CUs x 3 waves/SIMD.
-template <int D, int TS, bool DIRECT>
+// Register stages of an instantiation: pages above 8 KiB hold a whole stage
+// per page already (two would not fit the VGPR file).
+template <int D, int TS, int KVT>
+constexpr int split_stages() {
+  return TS * D * kv_elem_bytes<KVT>() > 8192 ? 1 : 2;
+}
+
+template <int D, int TS, bool DIRECT, int KVT>
 long long resident_waves() {
   static long long cached = 0;
   if (cached) return cached;
   int dev = 0, cus = 0, blocks = 0;
+  constexpr int ST = split_stages<D, TS, KVT>();
   if (hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, pa_split_kernel<D, TS, DIRECT>, 256, 0) ==
-          hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &blocks, pa_split_kernel<D, TS, DIRECT, 16384, kKvLoadAux, ST, 0, false, false, KVT>, 256,
+          0) == hipSuccess &&
       cus > 0 && blocks > 0) {
     cached = (long long)cus * blocks * 4;
   } else {
@@ -559,37 +599,77 @@ long long resident_waves() {
 // requested): same stream rate measured (scripts/tune_attention.py variant 6
 // vs 1), used when the launch must leave CU room for kernels running beside
 // it (micro-batch overlap).
-template <int D, int TS>
+template <int D, int TS, int KVT>
 hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_t st) {
   const int waves = ((a.B + a.group - 1) / a.group) * a.group * a.H * a.nsplit;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (a.group == 4 && !direct && !lean) {
+  if constexpr (KVT != LLM_F16) {
+    // other KV element types: the standard schedule (no lean / beam-prefetch forms)
+    constexpr int ST = split_stages<D, TS, KVT>();
+    if (direct)
+      hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 16384, kKvLoadAux, ST, 0, false, false, KVT>),
+                         grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false, KVT>),
+                         grid, block, 0, st, a);
+    return hipGetLastError();
+  }
+  constexpr int ST = split_stages<D, TS, LLM_F16>();
+  if (a.group == 4 && !direct && !lean && ST == 2) {
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, 2, 0, false, true>), grid,
                        block, 0, st, a);
-  } else if (lean) {
-    if (direct)
-      hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
-    else
-      hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
+  } else if (lean && TS * D * 2 <= 4096) {
+    // the 8-waves-per-SIMD register budget holds one stage of pages <= 4 KiB
+    if constexpr (TS * D * 2 <= 4096) {
+      if (direct)
+        hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
+      else
+        hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
+    }
   } else if (direct) {
-    hipLaunchKernelGGL((pa_split_kernel<D, TS, true>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 16384, kKvLoadAux, ST>), grid, block, 0, st, a);
   } else {
-    hipLaunchKernelGGL((pa_split_kernel<D, TS, false>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST>), grid, block, 0, st, a);
   }
   return hipGetLastError();
 }
 
-template <int D>
+template <int D, int KVT>
 hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, bool lean, hipStream_t st) {
-  switch (TS) {
-    case 16: return launch_split<D, 16>(a, direct, lean, st);
-    case 32: return launch_split<D, 32>(a, direct, lean, st);
+  constexpr int ES = kv_elem_bytes<KVT>();
+  if (TS == 16) {
+    if constexpr (kv_shape_ok(D, 16, ES)) return launch_split<D, 16, KVT>(a, direct, lean, st);
+  } else if (TS == 32) {
+    if constexpr (kv_shape_ok(D, 32, ES)) return launch_split<D, 32, KVT>(a, direct, lean, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int D>
+hipError_t dispatch_kvt(const PaSplitArgs& a, int kvt, int TS, bool direct, bool lean,
+                        hipStream_t st) {
+  switch (kvt) {
+    case LLM_F16: return dispatch_ts<D, LLM_F16>(a, TS, direct, lean, st);
+    case LLM_BF16: return dispatch_ts<D, LLM_BF16>(a, TS, direct, lean, st);
+    case LLM_F32: return dispatch_ts<D, LLM_F32>(a, TS, direct, lean, st);
+    case LLM_I8: return dispatch_ts<D, LLM_I8>(a, TS, direct, lean, st);
     default: return hipErrorInvalidValue;
   }
 }
 
-bool supported(int D, int TS) {
-  return (D == 32 || D == 64 || D == 128 || D == 256) && (TS == 16 || TS == 32);
+int kv_dtype_bytes(int kvt) {
+  switch (kvt) {
+    case LLM_F16: case LLM_BF16: return 2;
+    case LLM_F32: return 4;
+    case LLM_I8: return 1;
+    default: return 0;
+  }
+}
+
+bool supported(int D, int TS, int kvt) {
+  const int es = kv_dtype_bytes(kvt);
+  return es > 0 && (D == 32 || D == 64 || D == 128 || D == 256) && (TS == 16 || TS == 32) &&
+         kv_shape_ok(D, TS, es);
 }
 
 // Upper bound of the split count of any launch over rows of <= ntiles tiles
@@ -624,15 +704,31 @@ int choose_nsplit(int B, int H, int ntiles, int pps_fixed, long long resident) {
   return (int)std::min(ns, max_nsplit(B, H, ntiles));
 }
 
-template <int D, int TS>
-long long resident_for(bool direct) {
-  return direct ? resident_waves<D, TS, true>() : resident_waves<D, TS, false>();
+template <int D, int TS, int KVT>
+long long resident_for() {
+  if constexpr (kv_shape_ok(D, TS, kv_elem_bytes<KVT>()))
+    return resident_waves<D, TS, false, KVT>();
+  return 256LL * 4 * 3;
 }
 
-long long resident_waves_for(int D, int TS) {
+template <int D>
+long long resident_for_kvt(int TS, int kvt) {
+  auto by_ts = [&](auto k) -> long long {
+    constexpr int K = decltype(k)::value;
+    return TS == 16 ? resident_for<D, 16, K>() : resident_for<D, 32, K>();
+  };
+  switch (kvt) {
+    case LLM_BF16: return by_ts(std::integral_constant<int, LLM_BF16>{});
+    case LLM_F32: return by_ts(std::integral_constant<int, LLM_F32>{});
+    case LLM_I8: return by_ts(std::integral_constant<int, LLM_I8>{});
+    default: return by_ts(std::integral_constant<int, LLM_F16>{});
+  }
+}
+
+long long resident_waves_for(int D, int TS, int kvt) {
   auto pick = [&](auto d) -> long long {
     constexpr int DD = decltype(d)::value;
-    return TS == 16 ? resident_for<DD, 16>(false) : resident_for<DD, 32>(false);
+    return resident_for_kvt<DD>(TS, kvt);
   };
   switch (D) {
     case 32: return pick(std::integral_constant<int, 32>{});
@@ -682,15 +778,18 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   LLM_REQUIRE(!row_out || (size_t)H * D * 4 <= 65536, "pa_decode: row outputs need H*D <= 16384");
   LLM_REQUIRE(!rows || !rows->pack || (H * D) % 64 == 0, "pa_decode: packed row outputs need H*D % 64 == 0");
   LLM_REQUIRE(kv->k_pool && kv->v_pool && kv->page_table, "pa_decode: kv pointers NULL");
-  LLM_REQUIRE(kv->kv_dtype == LLM_F16, "pa_decode: only fp16 KV pools are supported");
+  LLM_REQUIRE(kv_dtype_bytes(kv->kv_dtype) > 0,
+              "pa_decode: kv_dtype must be LLM_F16, LLM_BF16, LLM_F32 or LLM_I8");
   LLM_REQUIRE(kv->num_heads == H, "pa_decode: H != kv->num_heads");
   LLM_REQUIRE(kv->head_dim == D, "pa_decode: D != kv->head_dim");
   LLM_REQUIRE(kv->num_pages > 0 && kv->num_beams > 0 && kv->max_tiles > 0,
               "pa_decode: empty kv view");
-  if (!supported(D, kv->page_size))
-    return fail(LLM_ERR_UNSUPPORTED, "pa_decode: unsupported head_dim/page_size (D in "
-                                     "{32,64,128,256}, page_size in {16,32})");
-  LLM_REQUIRE((long long)kv->num_pages * kv->page_size * D * 2 < (1LL << 47),
+  if (!supported(D, kv->page_size, kv->kv_dtype))
+    return fail(LLM_ERR_UNSUPPORTED, "pa_decode: unsupported head_dim/page_size/kv_dtype (D in "
+                                     "{32,64,128,256}, page_size in {16,32}, one page of "
+                                     "1..16 KiB)");
+  LLM_REQUIRE((long long)kv->num_pages * kv->page_size * D * kv_dtype_bytes(kv->kv_dtype) <
+                  (1LL << 47),
               "pa_decode: pool too large");
   const int TS = kv->page_size;
   // tiles at or past max_tiles have no page-table entry: they are missing (masked)
@@ -709,7 +808,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
       }
       resident = (long long)cus * 4 * std::min(waves_per_simd, 8);
     } else {
-      resident = resident_waves_for(D, TS);
+      resident = resident_waves_for(D, TS, kv->kv_dtype);
     }
   }
   const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
@@ -744,10 +843,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   hipError_t e;
   switch (D) {
-    case 32: e = dispatch_ts<32>(a, TS, direct, lean, st); break;
-    case 64: e = dispatch_ts<64>(a, TS, direct, lean, st); break;
-    case 128: e = dispatch_ts<128>(a, TS, direct, lean, st); break;
-    default: e = dispatch_ts<256>(a, TS, direct, lean, st); break;
+    case 32: e = dispatch_kvt<32>(a, kv->kv_dtype, TS, direct, lean, st); break;
+    case 64: e = dispatch_kvt<64>(a, kv->kv_dtype, TS, direct, lean, st); break;
+    case 128: e = dispatch_kvt<128>(a, kv->kv_dtype, TS, direct, lean, st); break;
+    default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, lean, st); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
   if (row_out && !direct) {

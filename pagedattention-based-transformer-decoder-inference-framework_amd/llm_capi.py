@@ -18,7 +18,7 @@ HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "libllm_decoder_hip.so"
 
 LLM_OK, LLM_ERR_INVALID, LLM_ERR_UNSUPPORTED, LLM_ERR_HIP, LLM_ERR_OOM, LLM_ERR_IO = range(6)
-LLM_F16, LLM_I8, LLM_F32 = 0, 1, 2
+LLM_F16, LLM_I8, LLM_F32, LLM_BF16 = 0, 1, 2, 3
 LLM_ACT_NONE, LLM_ACT_RELU, LLM_ACT_GELU = 0, 1, 2
 
 c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
@@ -68,6 +68,8 @@ _SIGS = {
                                 c_void_p, c_void_p, c_void_p]),
     "kv_cache_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_ll,
                                 ctypes.POINTER(c_void_p)]),
+    "kv_cache_create_typed": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_ll, c_int,
+                                      ctypes.POINTER(c_void_p)]),
     "kv_cache_destroy": (None, [c_void_p]),
     "kv_cache_view": (c_int, [c_void_p, c_int, ctypes.POINTER(PaKvView)]),
     "kv_cache_num_pages": (c_ll, [c_void_p]),
@@ -140,15 +142,27 @@ def ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
 
+def kv_dtype_of(t) -> int:
+    """llm_dtype of a torch KV pool tensor (fp16, bf16, fp32 or int8)."""
+    import torch
+    m = {torch.float16: LLM_F16, torch.bfloat16: LLM_BF16, torch.float32: LLM_F32,
+         torch.int8: LLM_I8}
+    if t.dtype not in m:
+        raise TypeError(f"KV pool dtype {t.dtype} is not one of fp16/bf16/fp32/int8")
+    return m[t.dtype]
+
+
 def kv_view(k_pool, v_pool, page_table, *, num_beams=None) -> PaKvView:
-    """View over torch device tensors k/v [num_pages][ts][D] fp16 and page
-    table int32 [num_beams][H][max_tiles]."""
+    """View over torch device tensors k/v [num_pages][ts][D] (fp16, bf16, fp32
+    or int8, both the same) and page table int32 [num_beams][H][max_tiles]."""
     nb, H, mt = page_table.shape
     v = PaKvView()
     v.k_pool, v.v_pool, v.page_table = k_pool.data_ptr(), v_pool.data_ptr(), page_table.data_ptr()
     v.num_pages, v.page_size, v.head_dim = k_pool.shape[0], k_pool.shape[1], k_pool.shape[2]
     v.num_beams, v.num_heads, v.max_tiles = num_beams or nb, H, mt
-    v.kv_dtype = LLM_F16
+    if k_pool.dtype != v_pool.dtype:
+        raise TypeError("k_pool and v_pool must have the same dtype")
+    v.kv_dtype = kv_dtype_of(k_pool)
     return v
 
 

@@ -25,6 +25,9 @@ ap.add_argument("--T", type=int, default=8192)
 ap.add_argument("--B", type=int, default=64)
 ap.add_argument("--interleave", action="store_true",
                 help="K and V of a page adjacent (one 2*page pool, K at even, V at odd pages)")
+ap.add_argument("--extent", type=int, default=1,
+                help="tiles per physically contiguous page run (1 = fully random pages; "
+                     "nt = each (row, head) contiguous)")
 args = ap.parse_args()
 B, H, D, T, ts = args.B, 16, 128, args.T, 16
 nt = (T + ts - 1) // ts
@@ -40,6 +43,11 @@ else:
     vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
     q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
     pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
+if args.extent > 1 and not args.interleave:
+    ext = args.extent
+    assert nt % ext == 0
+    runs = torch.randperm(num_pages // ext, generator=g, device="cuda").to(torch.int32)
+    pt = (runs[:, None] * ext + torch.arange(ext, device="cuda", dtype=torch.int32)).reshape(B, H, nt)
 lib = llm_capi.load()
 lib.pa_decode_tune.restype = ctypes.c_int
 lib.pa_decode_tune.argtypes = [ctypes.c_int, ctypes.POINTER(llm_capi.PaKvView), ctypes.c_void_p,

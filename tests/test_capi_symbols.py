@@ -60,6 +60,18 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.lm_head(None, None, None, 1, 10, 33, None) == 1
     assert lib.argmax_rows(None, 1, 10, None, None) == 1
     assert lib.kv_cache_create(0, 1, 1, 64, 16, 1, 1, ctypes.byref(ctypes.c_void_p())) == 1
+    assert lib.kv_cache_create_typed(1, 1, 1, 64, 16, 1, 1, 9, ctypes.byref(ctypes.c_void_p())) == 1
+    # KV element types: an unknown kv_dtype is invalid; a page outside 1..16 KiB
+    # (int8, D 32, 16 tokens = 512 B) is unsupported (fake pointers: rejected
+    # before anything is dereferenced)
+    fake = llm_capi.PaKvView(k_pool=1, v_pool=1, page_table=1, num_pages=1, page_size=16,
+                             head_dim=32, num_beams=1, num_heads=1, max_tiles=1,
+                             kv_dtype=llm_capi.LLM_I8)
+    args = (ctypes.c_void_p(1), ctypes.c_void_p(1), None, None, 1, 1, 32, 16, 1.0, 0, None, 0, None)
+    assert lib.pa_decode(ctypes.byref(fake), *args) == llm_capi.LLM_ERR_UNSUPPORTED
+    fake.kv_dtype = 9
+    assert lib.pa_decode(ctypes.byref(fake), *args) == llm_capi.LLM_ERR_INVALID
+    assert b"kv_dtype" in lib.llm_last_error()
     # zero-size work is a successful no-op
     assert lib.pa_decode(ctypes.byref(v), None, None, None, None, 0, 1, 64, 1, 1.0, 0, None, 0,
                          None) == 0

@@ -187,3 +187,73 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle):
             outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
                                       row_group=g).cpu().numpy()
             np.testing.assert_array_equal(outg, plain)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32", "int8"])
+def test_typed_kv_cache_attention_and_save_load(gpu, oracle, tmp_path, dtype):
+    """KVTileCache<T> for T in {bf16, float, int8_t} (kv_tile_cache.hpp:9):
+    tokens written through the typed cache, attention through the pybind11
+    paged_attention entry point, and a save/load round trip that keeps the
+    element type (a cache of another type refuses the file)."""
+    import torch
+    import llm_decoder
+    rng = np.random.default_rng(11)
+    H, D, TS, T, B = 2, 64, 16, 70, 2
+    dt = getattr(torch, dtype)
+    kv = llm_decoder.KVTileCache()
+    kv.init(num_pages=32, tile_size=TS, head_dim=D, num_layers=1, num_beams=B, num_heads=H,
+            max_tiles=8, dtype=dtype)
+    assert kv.view(0)["kv_dtype"] == {"bfloat16": 3, "float32": 2, "int8": 1}[dtype]
+    ks, vs = [], []
+    for b in range(B):
+        if dtype == "int8":
+            k = rng.integers(-4, 5, (T, H, D)).astype(np.int8)
+            v = rng.integers(-4, 5, (T, H, D)).astype(np.int8)
+            kf, vf = k.astype(np.float32), v.astype(np.float32)
+        else:
+            kt = torch.from_numpy(rng.standard_normal((T, H, D)).astype(np.float32) * 0.3).to(dt)
+            vt = torch.from_numpy(rng.standard_normal((T, H, D)).astype(np.float32)).to(dt)
+            kf, vf = kt.float().numpy(), vt.float().numpy()
+            k = kt.view(torch.int16).numpy() if dtype == "bfloat16" else kt.numpy()
+            v = vt.view(torch.int16).numpy() if dtype == "bfloat16" else vt.numpy()
+        kv.write_tokens(0, b, 0, k, v)
+        ks.append(kf)
+        vs.append(vf)
+    q = (rng.standard_normal((B, H, D)) * 0.1).astype(np.float32)
+    qd = torch.from_numpy(q).cuda()
+    out = torch.empty((B, H, D), device="cuda")
+    ws_bytes = llm_decoder.workspace_bytes(B, H, D, 8)
+    ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device="cuda")
+    kv.sync_page_table_to_gpu()
+    llm_decoder.paged_attention(kv.handle, 0, qd.data_ptr(), out.data_ptr(), B=B, H=H, D=D, T=T,
+                                workspace=ws.data_ptr(), workspace_bytes=ws_bytes)
+    torch.cuda.synchronize()
+    # oracle over a dense per-(beam, head) pool built from what was written
+    nt = (T + TS - 1) // TS
+    kpool = np.zeros((B * H * nt, TS, D), np.float32)
+    vpool = np.zeros_like(kpool)
+    pt = np.arange(B * H * nt, dtype=np.int32).reshape(B, H, nt)
+    for b in range(B):
+        for h in range(H):
+            for t in range(T):
+                kpool[pt[b, h, t // TS], t % TS] = ks[b][t, h]
+                vpool[pt[b, h, t // TS], t % TS] = vs[b][t, h]
+    ref = oracle.paged_attention(q, kpool, vpool, pt, T=T)
+    assert rel_err(out.cpu().numpy(), ref) < 1e-3
+    path = str(tmp_path / "kv.bin")
+    kv.save_to_file(path)
+    kv2 = llm_decoder.KVTileCache()
+    kv2.init(num_pages=32, tile_size=TS, head_dim=D, num_layers=1, num_beams=B, num_heads=H,
+             max_tiles=8, dtype=dtype)
+    kv2.load_from_file(path)
+    kv2.sync_page_table_to_gpu()
+    out2 = torch.empty_like(out)
+    llm_decoder.paged_attention(kv2.handle, 0, qd.data_ptr(), out2.data_ptr(), B=B, H=H, D=D,
+                                T=T, workspace=ws.data_ptr(), workspace_bytes=ws_bytes)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out)
+    other = llm_decoder.KVTileCache()
+    other.init(num_pages=32, tile_size=TS, head_dim=D, num_layers=1, num_beams=B, num_heads=H,
+               max_tiles=8, dtype="float16")
+    with pytest.raises(RuntimeError, match="kv_dtype"):
+        other.load_from_file(path)

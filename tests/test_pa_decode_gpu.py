@@ -211,3 +211,49 @@ def test_pa_decode_stale_nan_rows_ignored(gpu, oracle):
                                  pages_per_split=pps).cpu().numpy()
         assert np.isfinite(out).all()
         assert rel_err(out, ref) < RTOL
+
+
+def _kv_elems(rng, dtype, shape, scale):
+    """Random KV pool values exactly representable in `dtype`; returns (device
+    tensor, fp32 numpy copy the oracle reads)."""
+    import torch
+    if dtype == torch.int8:  # raw int8 values (KVTileCache<int8_t>, no scale)
+        a = rng.integers(-4, 5, size=shape).astype(np.int8)
+        return torch.from_numpy(a).cuda(), a.astype(np.float32)
+    t = torch.from_numpy((rng.standard_normal(shape) * scale).astype(np.float32)).to(dtype)
+    return t.cuda(), t.float().numpy()
+
+
+@pytest.mark.parametrize("kv_dtype", ["bfloat16", "float32", "int8", "float16"])
+@pytest.mark.parametrize("B,H,D,T,ts", [
+    (3, 4, 128, 1000, 16),
+    (2, 2, 64, 300, 32),
+    (2, 3, 256, 200, 16),
+    (5, 3, 32, 257, 32),
+])
+def test_pa_decode_kv_dtypes_vs_oracle(gpu, oracle, kv_dtype, B, H, D, T, ts):
+    """AttentionCUDA::forward's element types (attention/attention_cuda.cu:58-94:
+    __half, bf16, int8_t, float): pools of each type, every page 1..16 KiB.
+    The kernel widens each element to fp32 exactly, so the oracle reads the
+    same values as fp32 and the 1e-3 bound applies unchanged."""
+    import torch
+    import llm_capi
+    dt = getattr(torch, kv_dtype)
+    es = torch.empty(0, dtype=dt).element_size()
+    if not (1024 <= ts * D * es <= 16384):
+        pytest.skip("page size outside 1..16 KiB")
+    rng = np.random.default_rng(D * 7 + T + es)
+    nt = (T + ts - 1) // ts
+    num_pages = B * H * nt + 3
+    qs = 0.1 if dt == torch.int8 else D ** -0.25
+    q = (rng.standard_normal((B, H, D)) * qs).astype(np.float32)
+    kd, kf = _kv_elems(rng, dt, (num_pages, ts, D), D ** -0.25)
+    vd, vf = _kv_elems(rng, dt, (num_pages, ts, D), 1.0)
+    pt = rng.permutation(num_pages)[: B * H * nt].astype(np.int32).reshape(B, H, nt)
+    pt[0, 0, 1] = -1  # one missing page
+    lens = rng.integers(1, T + 1, size=B).astype(np.int32)
+    ref = oracle.paged_attention(q, kf, vf, pt, T=T, context_lens=lens)
+    for pps in (0, 4):
+        out = llm_capi.pa_decode(_dev(q), kd, vd, _dev(pt), T=T, context_lens=_dev(lens),
+                                 pages_per_split=pps).cpu().numpy()
+        assert rel_err(out, ref) < RTOL, (kv_dtype, pps, rel_err(out, ref))
