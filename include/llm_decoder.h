@@ -102,6 +102,38 @@ int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* out, const in
                       int pages_per_split, int row_group, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* The optional stages of the reference attention, CPUAttentionInput /
+ * CPUAttentionOutput (attention_cpu/attention_cpu.hpp:8-43) as used by
+ * cpu_paged_attention_forward (attention_cpu/cpu_attention_kernel.cpp:37-129):
+ *   scores_t = q.k_t / temperature (-1e9 where the tile is missing)
+ *   p = exp((scores - max) / temperature) / (sum + 1e-6)  (softmax_lut.cpp:203-231)
+ *   apply_topk_topp_filter (softmax_lut.cpp:233-256): rank by (p, index)
+ *     descending, zero rank >= top_k (top_k > 0) and every entry whose
+ *     higher-ranked mass is >= top_p (top_p < 1); no renormalisation; then if
+ *     eos_token >= 0 and p[eos_token] > eos_threshold, zero all other entries
+ *   out = sum_t p_t v_t
+ * The GPU kernel of the reference exposes the same knobs (top_k, top_p,
+ * rerank_scores: paged_flash_attention_kernel_fused.cu:5-90). */
+typedef struct pa_decode_options {
+  float temperature;   /* > 0; 1 = reference default (attention_config.hpp:20) */
+  int top_k;           /* 0 = off */
+  float top_p;         /* 1 = off */
+  int eos_token;       /* -1 = off (a KV position) */
+  float eos_threshold;
+  float* probs_out;    /* [B][H][T] attention weights after filtering, 0 past T_b (nullable) */
+  float* scores_out;   /* [B][H][T] scores, -1e9 past T_b / for missing tiles (nullable) */
+} pa_decode_options;
+
+/* pa_decode with the options above.  With every option off (top_k 0, top_p 1,
+ * eos -1, no outputs) this is pa_decode with sm_scale = 1/temperature^2 (the
+ * hot path; workspace as for pa_decode).  Otherwise one workgroup per (b, h)
+ * keeps the row's scores in LDS: T <= 8192 and D <= 256 (else
+ * LLM_ERR_UNSUPPORTED); workspace is unused. */
+int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
+                 const int32_t* context_lens, int B, int H, int D, int T,
+                 const pa_decode_options* opt, void* workspace, size_t workspace_bytes,
+                 void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* INT8 / FP16 weight GEMMs (MFMA)                                          */
 /* ------------------------------------------------------------------------ */

@@ -438,27 +438,39 @@ PYBIND11_MODULE(llm_decoder, m) {
         [](uintptr_t kv_handle, int layer, uintptr_t q, uintptr_t out, uintptr_t beam_ids,
            uintptr_t context_lens, int B, int H, int D, int T, float temperature, int top_k,
            float top_p, uintptr_t workspace, size_t workspace_bytes, uintptr_t stream,
-           int row_group) {
-          // AttentionCUDA::forward (attention/attention_cuda.cu:41-95) over a KVTileCache.
-          if (top_k > 0 || top_p < 1.0f)
-            throw std::runtime_error("paged_attention: top-k / top-p attention filters are not "
-                                     "supported on the GPU path (reference default is off)");
+           int row_group, int eos_token, float eos_threshold, uintptr_t probs_out,
+           uintptr_t scores_out) {
+          // AttentionCUDA::forward (attention/attention_cuda.cu:41-95) over a KVTileCache;
+          // the filters and weight / score outputs of CPUAttentionInput / Output
+          // (attention_cpu/attention_cpu.hpp:8-43) go through pa_decode_ex.
           pa_kv_view v;
           check(kv_cache_view(reinterpret_cast<kv_cache*>(kv_handle), layer, &v));
+          const auto* qp = reinterpret_cast<const float*>(q);
+          auto* op = reinterpret_cast<float*>(out);
+          const auto* bi = reinterpret_cast<const int32_t*>(beam_ids);
+          const auto* cl = reinterpret_cast<const int32_t*>(context_lens);
+          void* ws = reinterpret_cast<void*>(workspace);
+          void* st = reinterpret_cast<void*>(stream);
+          if (top_k > 0 || top_p < 1.0f || eos_token >= 0 || probs_out || scores_out) {
+            pa_decode_options o{temperature, top_k, top_p, eos_token, eos_threshold,
+                                reinterpret_cast<float*>(probs_out),
+                                reinterpret_cast<float*>(scores_out)};
+            py::gil_scoped_release nogil;
+            check(pa_decode_ex(&v, qp, op, bi, cl, B, H, D, T, &o, ws, workspace_bytes, st));
+            return;
+          }
           const float sm = 1.0f / (temperature * temperature);
           py::gil_scoped_release nogil;
-          check(pa_decode_grouped(&v, reinterpret_cast<const float*>(q),
-                                  reinterpret_cast<float*>(out),
-                                  reinterpret_cast<const int32_t*>(beam_ids),
-                                  reinterpret_cast<const int32_t*>(context_lens), B, H, D, T, sm,
-                                  0, row_group, reinterpret_cast<void*>(workspace),
-                                  workspace_bytes, reinterpret_cast<void*>(stream)));
+          check(pa_decode_grouped(&v, qp, op, bi, cl, B, H, D, T, sm, 0, row_group, ws,
+                                  workspace_bytes, st));
         },
         py::arg("kv_handle"), py::arg("layer"), py::arg("q"), py::arg("out"),
         py::arg("beam_ids") = 0, py::arg("context_lens") = 0, py::arg("B") = 1,
         py::arg("H") = 1, py::arg("D") = 64, py::arg("T") = 1, py::arg("temperature") = 1.0f,
         py::arg("top_k") = 0, py::arg("top_p") = 1.0f, py::arg("workspace") = 0,
-        py::arg("workspace_bytes") = 0, py::arg("stream") = 0, py::arg("row_group") = 1);
+        py::arg("workspace_bytes") = 0, py::arg("stream") = 0, py::arg("row_group") = 1,
+        py::arg("eos_token") = -1, py::arg("eos_threshold") = 0.0f, py::arg("probs_out") = 0,
+        py::arg("scores_out") = 0);
   m.def("workspace_bytes", &pa_decode_workspace_bytes, py::arg("B"), py::arg("H"), py::arg("D"),
         py::arg("max_tiles"), py::arg("pages_per_split") = 0);
 }

@@ -34,6 +34,13 @@ class PaKvView(ctypes.Structure):
                 ("kv_dtype", ctypes.c_int32)]
 
 
+class PaDecodeOptions(ctypes.Structure):
+    _fields_ = [("temperature", ctypes.c_float), ("top_k", ctypes.c_int),
+                ("top_p", ctypes.c_float), ("eos_token", ctypes.c_int),
+                ("eos_threshold", ctypes.c_float), ("probs_out", c_void_p),
+                ("scores_out", c_void_p)]
+
+
 class LlmError(RuntimeError):
     def __init__(self, status: int, msg: str):
         super().__init__(f"[llm status {status}] {msg}")
@@ -52,6 +59,9 @@ _SIGS = {
     "pa_decode_grouped": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_int, c_int, c_int, c_int, c_float, c_int, c_int,
                                   c_void_p, c_size_t, c_void_p]),
+    "pa_decode_ex": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_int, c_int, c_int, c_int, ctypes.POINTER(PaDecodeOptions),
+                             c_void_p, c_size_t, c_void_p]),
     "gemm_packed_bytes": (c_size_t, [c_int, c_int, c_int]),
     "gemm_pack_weights": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "i8_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -187,6 +197,29 @@ def pa_decode(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_lens=N
                             ptr(context_lens), B, H, D, T, sm_scale, pages_per_split, ptr(ws),
                             ws_bytes, stream_ptr(stream)))
     return out
+
+
+def pa_decode_ex(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_lens=None,
+                 temperature=1.0, top_k=0, top_p=1.0, eos_token=-1, eos_threshold=0.0,
+                 want_probs=False, stream=None):
+    """pa_decode_ex on torch device tensors.  Returns out [B][H][D] fp32, or
+    (out, probs [B][H][T], scores [B][H][T]) when want_probs."""
+    import torch
+    lib = load()
+    B, H, D = q.shape
+    out = torch.empty((B, H, D), dtype=torch.float32, device=q.device)
+    probs = torch.empty((B, H, T), dtype=torch.float32, device=q.device) if want_probs else None
+    scores = torch.empty((B, H, T), dtype=torch.float32, device=q.device) if want_probs else None
+    view = kv_view(k_pool, v_pool, page_table)
+    opt = PaDecodeOptions(temperature=temperature, top_k=top_k, top_p=top_p, eos_token=eos_token,
+                          eos_threshold=eos_threshold,
+                          probs_out=None if probs is None else probs.data_ptr(),
+                          scores_out=None if scores is None else scores.data_ptr())
+    ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, page_table.shape[2], 0)
+    ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=q.device)
+    check(lib.pa_decode_ex(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids), ptr(context_lens),
+                           B, H, D, T, ctypes.byref(opt), ptr(ws), ws_bytes, stream_ptr(stream)))
+    return (out, probs, scores) if want_probs else out
 
 
 def pack_weights(W, dtype: int, stream=None):

@@ -72,6 +72,17 @@ def test_invalid_arguments_rejected_before_any_launch():
     fake.kv_dtype = 9
     assert lib.pa_decode(ctypes.byref(fake), *args) == llm_capi.LLM_ERR_INVALID
     assert b"kv_dtype" in lib.llm_last_error()
+    # pa_decode_ex: temperature must be positive; the filtered kernel keeps a
+    # row of scores in LDS (T <= 8192)
+    fake.kv_dtype = llm_capi.LLM_F16
+    fake.head_dim = 64
+    opt = llm_capi.PaDecodeOptions(temperature=0.0, top_k=0, top_p=1.0, eos_token=-1)
+    exargs = (ctypes.c_void_p(1), ctypes.c_void_p(1), None, None, 1, 1, 64, 16)
+    assert lib.pa_decode_ex(ctypes.byref(fake), *exargs, ctypes.byref(opt), None, 0, None) == 1
+    opt.temperature, opt.top_k = 1.0, 5
+    big = exargs[:7] + (8193,)
+    assert lib.pa_decode_ex(ctypes.byref(fake), *big, ctypes.byref(opt), None, 0,
+                            None) == llm_capi.LLM_ERR_UNSUPPORTED
     # zero-size work is a successful no-op
     assert lib.pa_decode(ctypes.byref(v), None, None, None, None, 0, 1, 64, 1, 1.0, 0, None, 0,
                          None) == 0

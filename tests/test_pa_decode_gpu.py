@@ -257,3 +257,112 @@ def test_pa_decode_kv_dtypes_vs_oracle(gpu, oracle, kv_dtype, B, H, D, T, ts):
         out = llm_capi.pa_decode(_dev(q), kd, vd, _dev(pt), T=T, context_lens=_dev(lens),
                                  pages_per_split=pps).cpu().numpy()
         assert rel_err(out, ref) < RTOL, (kv_dtype, pps, rel_err(out, ref))
+
+
+FILTER_CASES = ["topk5", "topp09", "eos", "c1_base", "c1_missing", "beam_route", "temp07",
+                "ragged_tail", "ts32", "all_missing"]
+
+
+def _check_scores(got, want):
+    missing = want <= -1e8
+    np.testing.assert_array_equal(got[missing], np.full(missing.sum(), -1e9, np.float32))
+    if (~missing).any():
+        assert rel_err(got[~missing], want[~missing]) < RTOL
+
+
+@pytest.mark.parametrize("name", FILTER_CASES)
+def test_pa_decode_ex_matches_golden(gpu, oracle, name):
+    """The reference's optional attention stages (top-k, top-p, EOS threshold,
+    attention-weight and score outputs; CPUAttentionInput / Output,
+    attention_cpu/attention_cpu.hpp:8-43) against the reference-built golden
+    fixtures, which hold out, probs (after the filter) and scores."""
+    import llm_capi
+    f = load_attn_fixture(name)
+    k_pool, v_pool, pt = tiles_to_pool(f["k"], f["v"], f["present"])
+    bi = None if f["beam_ids"] is None else _dev(f["beam_ids"])
+    out, probs, scores = llm_capi.pa_decode_ex(
+        _dev(f["q"]), _dev(k_pool), _dev(v_pool), _dev(pt), T=f["T"], beam_ids=bi,
+        temperature=f["temperature"], top_k=f["top_k"], top_p=f["top_p"], eos_token=f["eos"],
+        eos_threshold=f["eos_thr"], want_probs=True)
+    out, probs, scores = (x.cpu().numpy() for x in (out, probs, scores))
+    if name == "all_missing":
+        np.testing.assert_array_equal(out, np.zeros_like(out))
+    else:
+        assert rel_err(out, f["out"]) < RTOL, rel_err(out, f["out"])
+    assert rel_err(probs, f["probs"]) < RTOL
+    # the filter keeps exactly the reference's set of positions
+    np.testing.assert_array_equal(probs > 0, f["probs"] > 0)
+    _check_scores(scores, f["scores"])
+
+
+@pytest.mark.parametrize("kv_dtype", ["float16", "bfloat16", "float32", "int8"])
+@pytest.mark.parametrize("top_k,top_p,eos", [(0, 1.0, -1), (7, 1.0, -1), (0, 0.6, -1),
+                                             (20, 0.8, -1), (0, 1.0, 3)])
+def test_pa_decode_ex_random_vs_oracle(gpu, oracle, kv_dtype, top_k, top_p, eos):
+    """Filters on ragged rows with beam routing and missing pages, every KV
+    element type, against the oracle's restatement of apply_topk_topp_filter."""
+    import torch
+    import llm_capi
+    dt = getattr(torch, kv_dtype)
+    rng = np.random.default_rng(top_k * 31 + eos + 5)
+    B, H, D, T, ts, beams = 4, 3, 64, 700, 16, 3
+    nt = (T + ts - 1) // ts
+    num_pages = beams * H * nt + 2
+    temp = 0.8
+    q = (rng.standard_normal((B, H, D)) * (0.1 if dt == torch.int8 else 0.5)).astype(np.float32)
+    kd, kf = _kv_elems(rng, dt, (num_pages, ts, D), 0.5)
+    vd, vf = _kv_elems(rng, dt, (num_pages, ts, D), 1.0)
+    pt = rng.permutation(num_pages)[: beams * H * nt].astype(np.int32).reshape(beams, H, nt)
+    pt[1, 2, 3] = -1
+    beam_ids = np.array([2, 0, 1, 2], np.int32)
+    lens = np.array([700, 1, 333, 650], np.int32)
+    ref, rp, rs = oracle.paged_attention(q, kf, vf, pt, T=T, beam_ids=beam_ids, context_lens=lens,
+                                         temperature=temp, top_k=top_k, top_p=top_p,
+                                         eos_token=eos, eos_threshold=0.0, want_probs=True)
+    out, probs, scores = llm_capi.pa_decode_ex(
+        _dev(q), kd, vd, _dev(pt), T=T, beam_ids=_dev(beam_ids), context_lens=_dev(lens),
+        temperature=temp, top_k=top_k, top_p=top_p, eos_token=eos, eos_threshold=0.0,
+        want_probs=True)
+    out, probs, scores = (x.cpu().numpy() for x in (out, probs, scores))
+    assert rel_err(out, ref) < RTOL
+    assert rel_err(probs, rp) < RTOL
+    np.testing.assert_array_equal(probs > 0, rp > 0)
+    _check_scores(scores, rs)
+    if top_k == 0 and top_p >= 1.0 and eos < 0:  # no stage active: same as the hot path
+        hot = llm_capi.pa_decode(_dev(q), kd, vd, _dev(pt), T=T, beam_ids=_dev(beam_ids),
+                                 context_lens=_dev(lens), sm_scale=1.0 / temp ** 2).cpu().numpy()
+        assert rel_err(hot, out) < RTOL
+
+
+def test_paged_attention_binding_filters(gpu, oracle):
+    """llm_decoder.paged_attention (AttentionCUDA::forward surface) with top_k /
+    top_p now runs the filtered kernel instead of refusing."""
+    import torch
+    import llm_decoder
+    rng = np.random.default_rng(2)
+    H, D, TS, T = 2, 64, 16, 90
+    kv = llm_decoder.KVTileCache()
+    kv.init(num_pages=32, tile_size=TS, head_dim=D, num_layers=1, num_beams=1, num_heads=H,
+            max_tiles=8)
+    k = (rng.standard_normal((T, H, D)) * 0.4).astype(np.float16)
+    v = rng.standard_normal((T, H, D)).astype(np.float16)
+    kv.write_tokens(0, 0, 0, k.view(np.uint16), v.view(np.uint16))
+    kv.sync_page_table_to_gpu()
+    q = (rng.standard_normal((1, H, D)) * 0.5).astype(np.float32)
+    qd = torch.from_numpy(q).cuda()
+    out = torch.empty((1, H, D), device="cuda")
+    probs = torch.empty((1, H, T), device="cuda")
+    llm_decoder.paged_attention(kv.handle, 0, qd.data_ptr(), out.data_ptr(), B=1, H=H, D=D, T=T,
+                                top_k=10, top_p=0.9, probs_out=probs.data_ptr())
+    torch.cuda.synchronize()
+    nt = (T + TS - 1) // TS
+    pt = np.arange(H * nt, dtype=np.int32).reshape(1, H, nt)
+    kp = np.zeros((H * nt, TS, D), np.float32)
+    vp = np.zeros_like(kp)
+    for h in range(H):
+        for t in range(T):
+            kp[pt[0, h, t // TS], t % TS] = k[t, h]
+            vp[pt[0, h, t // TS], t % TS] = v[t, h]
+    ref, rp, _ = oracle.paged_attention(q, kp, vp, pt, T=T, top_k=10, top_p=0.9, want_probs=True)
+    assert rel_err(out.cpu().numpy(), ref) < RTOL
+    np.testing.assert_array_equal(probs.cpu().numpy() > 0, rp > 0)
