@@ -128,6 +128,7 @@ struct llm_decoder {
   std::vector<hipEvent_t> ev_attn;  // [L][2]
   DevBuf<uint8_t> attn_ws2;
   int qa_ld = 0;
+  size_t b16 = 0;  // max_batch rounded up to 16-row tiles
 
   int layer_pre(int l, hipStream_t st, const struct Rows& R);
   int layer_attn(int l, hipStream_t st, const struct Rows& R);
@@ -193,7 +194,8 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->sa.alloc((size_t)B));
   const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
   RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
-  if (d->wdtype == LLM_F16) RET_IF(d->a16.alloc(B16 * std::max(hid, inter)));
+  if (d->wdtype == LLM_F16) RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
+  d->b16 = B16;
   RET_IF(d->tokens.alloc((size_t)B));
   RET_IF(d->pos.alloc((size_t)B));
   RET_IF(d->ctx.alloc((size_t)B));
@@ -340,6 +342,7 @@ struct Rows {
   float* o = nullptr;   // [n][hid] attention output (fp32)
   float* h1 = nullptr;  // [n][inter]
   void* act = nullptr;  // packed-A GEMM input (int8 or fp16), 16-row tiles
+  void* act2 = nullptr; // fp16 decoder: fc2's packed input (written by fc1 while act is read)
   float* sa = nullptr;  // [n] int8 row scales
   const int32_t* pos = nullptr;  // [n] position written this pass
   const int32_t* ctx = nullptr;  // [n] context length attended (pos + 1)
@@ -428,15 +431,23 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
                                        static_cast<int8_t*>(R.act), R.sa, st, 1));
   else
     LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, R.act, st, 1));
-  g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid; g.C = R.h1;
+  g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
-  if (i8) g.sw = sw1.p + (size_t)l * inter;
+  if (i8) {
+    g.C = R.h1;
+    g.sw = sw1.p + (size_t)l * inter;
+  } else {
+    // fp16 decoder: the fc1 epilogue writes fc2's packed fp16 input directly
+    // (no per-row scale to wait for, so no conversion launch)
+    g.C = nullptr;
+    g.C16 = R.act2;
+  }
   RET_IF(weight_gemm(g, st));
+  g.C16 = nullptr;
+  if (!i8) g.A = R.act2;
   // quantise h1 -> mlp_fc2 (+b2)
   if (i8)
     LLM_HIP_RET(launch_quantize_rows(R.h1, R.n, inter, static_cast<int8_t*>(R.act), R.sa, st, 1));
-  else
-    LLM_HIP_RET(launch_to_f16(R.h1, (size_t)R.n * inter, R.act, st, inter));
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
@@ -452,6 +463,7 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
   R.o = o.p + (size_t)r0 * hid;
   R.h1 = h1.p + (size_t)r0 * inter;
   R.act = wdtype == LLM_I8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
+  if (wdtype == LLM_F16) R.act2 = a16.p + (b16 + (size_t)r0) * qa_ld;
   R.sa = sa.p + r0;
   R.pos = pos.p + r0;
   R.ctx = ctx.p + r0;
@@ -609,7 +621,7 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     RET_IF(po.alloc((size_t)C * hid));
     RET_IF(ph1.alloc((size_t)C * inter));
     RET_IF(psa.alloc((size_t)C));
-    RET_IF(pact.alloc(C16 * std::max(hid, inter) * (wdtype == LLM_I8 ? 1 : 2)));
+    RET_IF(pact.alloc(C16 * std::max(hid, inter) * (wdtype == LLM_I8 ? 1 : 4)));  // F16: act, act2
     RET_IF(pmeta.alloc((size_t)4 * C));
     pws_bytes = 16;
     for (int b = 1; b <= C; ++b)
@@ -638,6 +650,8 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     Rows R;
     R.n = m;
     R.x = px.p; R.q = pq.p; R.o = po.p; R.h1 = ph1.p; R.act = pact.p; R.sa = psa.p;
+    if (wdtype == LLM_F16)
+      R.act2 = pact.p + (((size_t)C + 15) / 16 * 16) * std::max(hid, inter) * 2;
     R.pos = pmeta.p; R.ctx = pmeta.p + C; R.beam_rows = pmeta.p + 2 * C;
     R.attn_ws = pws.p; R.attn_ws_bytes = pws_bytes;
     LLM_HIP_RET(launch_embed(emb.p, pmeta.p + 3 * C, m, hid, V, px.p, st));

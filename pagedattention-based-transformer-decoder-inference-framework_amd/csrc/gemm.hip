@@ -54,6 +54,7 @@ struct GemmArgs {
   int32_t* acc_out;
   int c_cols;         // columns of C actually stored (< N with a KV append: q only)
   int c_ld;           // row stride of C
+  _Float16* c16;      // optional fp16 copy of C in packed-A order (the next GEMM's input)
   KvAppend kv;        // kv.k_pool == nullptr: no append
 };
 
@@ -280,6 +281,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     }
     y = apply_act(y, a.act);
     if (a.C && n < a.c_cols) a.C[(size_t)m * a.c_ld + n] = y;
+    if (a.c16) a.c16[a_frag_off_f16(m, n, a.N >> 5)] = (_Float16)y;
     if (e_page[e] >= 0) {
       const int which = n >= 2 * hid;  // 0: K, 1: V
       const int i = n - hid * (1 + which);
@@ -457,6 +459,8 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.C = g.C;
   a.c_cols = g.c_cols > 0 ? g.c_cols : g.N;
   a.c_ld = g.c_ld > 0 ? g.c_ld : g.N;
+  LLM_REQUIRE(!g.C16 || g.N % 32 == 0, "weight_gemm: packed fp16 output needs N % 32 == 0");
+  a.c16 = static_cast<_Float16*>(g.C16);
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");

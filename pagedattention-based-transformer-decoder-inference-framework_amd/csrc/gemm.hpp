@@ -36,8 +36,9 @@ struct WeightGemm {
   const float* sw = nullptr;
   const float* bias = nullptr;
   int act = LLM_ACT_NONE;
-  float* C = nullptr;
+  float* C = nullptr;         // may be NULL when C16 is the only output
   int c_cols = 0, c_ld = 0;  // 0: N
+  void* C16 = nullptr;       // fp16 copy of C in packed-A order with K = N (next GEMM's input)
   const KvAppendView* kv = nullptr;
 };
 
