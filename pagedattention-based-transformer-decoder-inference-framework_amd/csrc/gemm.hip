@@ -56,14 +56,24 @@ struct GemmArgs {
   int c_ld;           // row stride of C
   _Float16* c16;      // optional fp16 copy of C in packed-A order (the next GEMM's input)
   KvAppend kv;        // kv.k_pool == nullptr: no append
+  unsigned long long* stamps;  // diagnostics only (i8_gemm_stamps): per-workgroup phase clocks
 };
+
+// Phase clock (100 MHz s_memrealtime) of the diagnostic build path.
+__device__ __forceinline__ unsigned long long phase_clock() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
 
 
 // k-steps per pipeline batch (two batches in flight): bounded by the VGPRs of
 // the A fragments (MT tiles, x2 for the fp32 LM-head A) held per k-step.
-template <int MT>
+template <int MT, int WAVES>
 constexpr int gemm_unroll() {
-  return MT >= 4 ? 2 : 4;
+  // 4-wave workgroups carry twice the k-steps per wave: twice the batch, so
+  // the same bytes are in flight from half the waves
+  return (MT >= 4 ? 2 : 4) * (WAVES == 4 ? 2 : 1);
 }
 
 __device__ __forceinline__ float apply_act(float y, int act) {
@@ -80,11 +90,13 @@ template <>
 struct GemmTraits<GemmKind::I8> {
   static constexpr int KSTEP = 64, ESIZE = 1;
   using acc_t = i32x4;
+  using elem_t = int32_t;
 };
 template <>
 struct GemmTraits<GemmKind::F16> {
   static constexpr int KSTEP = 32, ESIZE = 2;
   using acc_t = f32x4;
+  using elem_t = float;
 };
 
 // One workgroup = NT consecutive 16-column tiles x 16*MT rows; its 8 waves
@@ -93,20 +105,33 @@ struct GemmTraits<GemmKind::F16> {
 // L2, instead of MT:1), and the k loop is software-pipelined in batches of
 // kUnroll k-steps: batch i+1's loads are in flight while batch i's MFMAs run.
 // Weight loads are non-temporal (each weight byte is read once per step).
-template <GemmKind KIND, int MT, int NT, int WAVES>
+// DIAG (diagnostics only, i8_gemm_stamps): bit 0 = no A loads (A reads as
+// zero), bit 1 = no epilogue (wave 0 stores one word per workgroup).
+template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0>
 __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   using Tr = GemmTraits<KIND>;
   using acc_t = typename Tr::acc_t;
   constexpr int KSTEP = Tr::KSTEP;
-  constexpr int kUnroll = gemm_unroll<MT>();
-  __shared__ __attribute__((aligned(16))) acc_t red[WAVES][MT * NT][64];
+  constexpr int kUnroll = gemm_unroll<MT, WAVES>();
+  // Cross-wave partial sums, [wave][tile][reg][lane]: lane-fastest so both the
+  // per-register stores and the epilogue's reads (consecutive threads =
+  // consecutive columns = consecutive lanes) are bank-conflict free.
+  using elem_t = typename Tr::elem_t;
+  __shared__ elem_t red[WAVES][MT * NT][4][64];
 
   const int lane = lane_id();
   const int w = wave_id_uniform();
   const int nt0 = blockIdx.x * NT;
   const int m0 = blockIdx.y * 16 * MT;
-  const int ks0 = (w * a.KS) / WAVES;
-  const int ks1 = ((w + 1) * a.KS) / WAVES;
+  unsigned long long* stamp =
+      a.stamps ? a.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 48 : nullptr;
+  if (stamp && lane == 0) stamp[w] = phase_clock();  // [0, 16): wave start
+  // Wave w streams k range wr = (w + blockIdx.x) % WAVES: at any moment the
+  // workgroups of an XCD read different A fragments (all of them read all of
+  // A), instead of every workgroup hitting the same L2 lines.
+  const int wr = (w + blockIdx.x) % WAVES;
+  const int ks0 = (wr * a.KS) / WAVES;
+  const int ks1 = ((wr + 1) * a.KS) / WAVES;
   const int ntiles = (a.N + 15) >> 4;
 
   // A descriptor: rows >= M (and anything past the matrix) read as zero.
@@ -161,7 +186,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       for (int mt = 0; mt < MT; ++mt) {
         const uint32_t koff = (uint32_t)kk * a_kstride + a_kgrp_off;
         const uint32_t aoff = (ok && a_row_off[mt] != 0xFFFFFFF0u) ? a_row_off[mt] + koff : 0xFFFFFFF0u;
-        bt.af[u][mt] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff, 0, 0);
+        if constexpr ((DIAG & 1) != 0)
+          bt.af[u][mt] = u32x4{aoff, 0u, 0u, 0u};
+        else
+          bt.af[u][mt] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff, 0, 0);
       }
     }
   };
@@ -243,10 +271,23 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     }
   }
 
+  if (stamp && lane == 0) stamp[16 + w] = phase_clock();  // [16, 32): k loop done
+  if constexpr ((DIAG & 2) != 0) {
+    int32_t x = 0;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) x ^= (int32_t)acc[mt][j][0] ^ (int32_t)acc[mt][j][3];
+    if (lane == 0 && a.C) a.C[blockIdx.x] = (float)x;
+    if (stamp && lane == 0) stamp[32 + w] = phase_clock();
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) red[w][mt * NT + j][lane] = acc[mt][j];
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wr][mt * NT + j][r][lane] = acc[mt][j][r];
   __syncthreads();
 
 #pragma unroll
@@ -269,14 +310,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     if constexpr (KIND == GemmKind::I8) {
       int32_t s = 0;
 #pragma unroll
-      for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][src_lane][reg];
+      for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][reg][src_lane];
       if (a.acc_out) a.acc_out[(size_t)m * a.N + n] = s;
       y = (float)s * e_scale[e];
       if (a.bias) y = y + e_bias[e];
     } else {
       float s = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][src_lane][reg];
+      for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][reg][src_lane];
       y = a.bias ? s + e_bias[e] : s;
     }
     y = apply_act(y, a.act);
@@ -291,6 +332,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       (which ? kv.v_pool : kv.k_pool)[off] = (_Float16)y;
     }
   }
+  if (stamp && lane == 0) stamp[32 + w] = phase_clock();  // [32, 48): wave end
 }
 
 // Repack W [K][N] (row-major) into per-(16-col tile, k-step) 1 KiB blocks,
@@ -330,8 +372,8 @@ template <GemmKind KIND, int MT, int NT>
 hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t st) {
   const int ntiles = (a.N + 15) / 16;
   const dim3 grid((ntiles + NT - 1) / NT, mblocks);
-  if (waves == 16)
-    hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 16>), grid, dim3(1024), 0, st, a);
+  if (waves == 4)
+    hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 4>), grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8>), grid, dim3(512), 0, st, a);
   return hipGetLastError();
@@ -343,9 +385,8 @@ hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hip
                  : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st);
 }
 
-// Waves per workgroup (they split K): 8.  The 16-wave form (1024 threads)
-// caps the kernel at 128 VGPRs and spills (scripts/kernel_resources.py); it is
-// kept for the tuning entry only.
+// Waves per workgroup (they split K): 8.  The 4-wave form (twice the
+// k-steps per wave) is kept for the tuning entry.
 inline int pick_waves(const GemmArgs&, int) { return 8; }
 
 template <GemmKind KIND>
@@ -476,6 +517,55 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
 
 // Tuning hook (not in include/llm_decoder.h): i8_gemm with a forced column-tile
 // count, waves per workgroup and rows per workgroup (16 / 32 / 64; 0 = auto).
+// Diagnostic (not in include/llm_decoder.h): i8_gemm_tune with per-workgroup
+// phase clocks, stamps[wg][0..16) wave start, [16..32) k loop done, [32..48) wave end, plus one
+// launch-end clock per workgroup in ends[wg] (100 MHz ticks).
+__global__ void gemm_end_stamp_kernel(unsigned long long* t) {
+  if (threadIdx.x == 0) *t = phase_clock();
+}
+
+extern "C" int i8_gemm_stamps(int nt, int waves, int mrows, const int8_t* A, const void* W_packed,
+                              float* C, int M, int N, int K, const float* sa, const float* sw,
+                              unsigned long long* stamps, unsigned long long* end_stamp,
+                              void* stream) {
+  GemmArgs a{};
+  a.a_packed = 1;
+  a.A = reinterpret_cast<const uint8_t*>(A);
+  a.lda = K;
+  a.B = static_cast<const uint8_t*>(W_packed);
+  a.M = M; a.N = N; a.K = K; a.KS = K / 64;
+  a.sa = sa; a.sw = sw; a.C = C; a.c_cols = N; a.c_ld = N;
+  a.stamps = stamps;
+  hipStream_t st = as_stream(stream);
+  hipError_t e = hipSuccess;
+  const int ntiles = N / 16;
+  const int diag = waves >> 8;  // waves = 8 | (diag << 8)
+  if (diag == 0) {
+    e = launch_gemm<GemmKind::I8>(a, st, nt, waves, mrows);
+  } else {
+    // diagnostic forms of the two production shapes only
+    LLM_REQUIRE((nt == 2 && mrows == 64) || (nt == 1 && mrows == 32), "i8_gemm_stamps: diag shape");
+    auto go = [&](auto kern, int NTv, int mr) {
+      hipLaunchKernelGGL(kern, dim3((ntiles + NTv - 1) / NTv, (M + mr - 1) / mr), dim3(512), 0, st, a);
+    };
+    if (nt == 2) {
+      if (diag == 1) go(gemm_kernel<GemmKind::I8, 4, 2, 8, 1>, 2, 64);
+      else if (diag == 2) go(gemm_kernel<GemmKind::I8, 4, 2, 8, 2>, 2, 64);
+      else go(gemm_kernel<GemmKind::I8, 4, 2, 8, 3>, 2, 64);
+    } else {
+      if (diag == 1) go(gemm_kernel<GemmKind::I8, 2, 1, 8, 1>, 1, 32);
+      else if (diag == 2) go(gemm_kernel<GemmKind::I8, 2, 1, 8, 2>, 1, 32);
+      else go(gemm_kernel<GemmKind::I8, 2, 1, 8, 3>, 1, 32);
+    }
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(gemm_end_stamp_kernel, dim3(1), dim3(64), 0, st, end_stamp);
+    e = hipGetLastError();
+  }
+  return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_stamps");
+}
+
 extern "C" int i8_gemm_tune(int nt, int waves, int mrows, int a_packed, const int8_t* A, int lda,
                             const void* W_packed, float* C, int M, int N, int K, const float* sa,
                             const float* sw, void* stream) {

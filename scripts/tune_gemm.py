@@ -43,7 +43,7 @@ for name, K, N in shapes:
     llm_capi.check(lib.i8_gemm_tune(1, 8, 0, 0, A.data_ptr(), K, Wp.data_ptr(),
                                     ref.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(), None))
     for nt, ks, apk, mr in [(1, 8, 1, 64), (2, 8, 1, 64), (1, 8, 1, 32), (2, 8, 1, 32),
-                            (1, 8, 1, 16), (1, 16, 1, 32)]:
+                            (1, 8, 1, 16), (2, 4, 1, 64), (1, 4, 1, 32), (1, 4, 1, 16)]:
         for _ in range(1):
             C.zero_()
             llm_capi.check(lib.i8_gemm_tune(nt, ks, mr, apk, (Ap if apk else A).data_ptr(), K,
