@@ -212,7 +212,12 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   // one batch 3607-3621; two free-running halves 3672-3674 (+1.5 %, within
   // box-to-box spread, and 7 % slower under rocprofv3's kernel trace);
   // ping-pong attention 3156-3592 — the glue kernels slow 4-8x beside a
-  // saturating KV scan, so the overlap does not pay on this path.
+  // saturating KV scan, so the overlap does not pay on this path.  A CU
+  // partition (attention and glue on hipExtStreamCreateWithCUMask streams,
+  // 16/32/48 glue CUs, eager) measured 2485-2645: the weight GEMMs are paced
+  // per CU (~6 GB/s per CU), so 32 CUs need ~275 us of glue per half-layer,
+  // the half-batch scan on 224 CUs runs 9 % slower (365 vs 335 us) and each
+  // cross-stream event adds ~13 us.
   d->microbatches = env_int("LLM_MICROBATCHES", 1);
   d->pingpong = env_int("LLM_MB_PINGPONG", 0) != 0;
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
