@@ -64,6 +64,10 @@ typedef struct pa_kv_view {
   int32_t max_tiles;
   int32_t kv_dtype;           /* LLM_F16 (default), LLM_BF16, LLM_F32 or LLM_I8; one page
                                * (page_size * head_dim elements) must be 1..16 KiB */
+  int64_t page_stride;        /* bytes from page p to page p + 1 within each pool; 0 = one
+                               * page (dense pools).  kv_cache's own pools interleave K and
+                               * V pages ([num_pages][K page | V page], stride 2 pages,
+                               * v_pool = k_pool + 1 page) */
 } pa_kv_view;
 
 /* Bytes of device workspace pa_decode needs (split-T partial softmax state). */
@@ -235,9 +239,11 @@ int kv_cache_sync(kv_cache* c, void* stream);
  * `beam` starting at token position pos into the pools of `layer`. */
 int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, int n, const void* k_host,
                           const void* v_host);
-/* Device pointers of the pools / table (for tests and custom kernels). */
+/* Device pointers of the pools / table (for tests and custom kernels).  Page
+ * p of the K (V) pool starts at kv_cache_k_pool (v_pool) + p * page_stride. */
 void* kv_cache_k_pool(kv_cache* c);
 void* kv_cache_v_pool(kv_cache* c);
+long long kv_cache_page_stride(const kv_cache* c);
 int32_t* kv_cache_page_table(kv_cache* c, int layer);
 /* KVTileCache::save_to_file / load_from_file (kv_tile_cache.cpp:105-125):
  * header + page table + used pages. */

@@ -264,12 +264,12 @@ class KVTileCache {
   uintptr_t get_key_ptr(int page) const {
     need();
     if (page < 0 || page >= kv_cache_num_pages(c_)) throw std::out_of_range("page id");
-    return reinterpret_cast<uintptr_t>(kv_cache_k_pool(c_)) + (uintptr_t)page * tile_size_ * head_dim_ * es_;
+    return reinterpret_cast<uintptr_t>(kv_cache_k_pool(c_)) + (uintptr_t)page * kv_cache_page_stride(c_);
   }
   uintptr_t get_value_ptr(int page) const {
     need();
     if (page < 0 || page >= kv_cache_num_pages(c_)) throw std::out_of_range("page id");
-    return reinterpret_cast<uintptr_t>(kv_cache_v_pool(c_)) + (uintptr_t)page * tile_size_ * head_dim_ * es_;
+    return reinterpret_cast<uintptr_t>(kv_cache_v_pool(c_)) + (uintptr_t)page * kv_cache_page_stride(c_);
   }
   int register_tile(int beam, int head, int tile, int layer) {
     need();
@@ -309,6 +309,7 @@ class KVTileCache {
     d["num_pages"] = v.num_pages; d["page_size"] = v.page_size; d["head_dim"] = v.head_dim;
     d["num_beams"] = v.num_beams; d["num_heads"] = v.num_heads; d["max_tiles"] = v.max_tiles;
     d["kv_dtype"] = v.kv_dtype;
+    d["page_stride"] = v.page_stride;
     return d;
   }
   long long free_pages() const { need(); return kv_cache_free_pages(c_); }

@@ -5,11 +5,18 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "llm_decoder.h"
 
 namespace llm {
+
+// Integer tuning knob from the environment (dflt when unset or empty).
+inline int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
 
 // Thread-local last-error message (llm_last_error()).
 void set_error(const std::string& msg);

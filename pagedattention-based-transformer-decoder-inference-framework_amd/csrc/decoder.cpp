@@ -58,11 +58,6 @@ struct DevBuf {
 
 #define RET_IF(x) do { int _rc = (x); if (_rc) return _rc; } while (0)
 
-int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return (v && *v) ? std::atoi(v) : dflt;
-}
-
 }  // namespace
 
 struct llm_decoder {
@@ -381,6 +376,7 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   app.num_pages = view.num_pages;
   app.H = H;
   app.D = D;
+  app.page_stride = (size_t)view.page_stride / sizeof(_Float16);
   WeightGemm g;
   g.dtype = wdtype;
   g.a_packed = 1;
@@ -712,9 +708,9 @@ extern "C" int llm_decoder_begin_synthetic(llm_decoder* d, int batch, int contex
   for (int b = 0; b < batch; ++b) RET_IF(kv_cache_reserve(d->kv, b, context_len));
   RET_IF(kv_cache_sync(d->kv, d->stream));
   // seeded random fp16 K/V over the whole pools (K scaled so q.k ~ O(1))
-  const size_t n = (size_t)k->num_pages * k->page_elems;
-  LLM_HIP_RET(launch_fill_random_f16(k->k_pool, n, seed * 2 + 1, 0.05f, d->stream));
-  LLM_HIP_RET(launch_fill_random_f16(k->v_pool, n, seed * 2 + 2, 1.0f, d->stream));
+  const size_t np = (size_t)k->num_pages, pe = k->page_elems, ps = k->page_stride() / k->es;
+  LLM_HIP_RET(launch_fill_random_f16(k->k_pool, np, pe, ps, seed * 2 + 1, 0.05f, d->stream));
+  LLM_HIP_RET(launch_fill_random_f16(k->v_pool, np, pe, ps, seed * 2 + 2, 1.0f, d->stream));
   LLM_HIP_RET(hipStreamSynchronize(d->stream));
   return LLM_OK;
 }
@@ -748,9 +744,9 @@ extern "C" int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_wi
     for (int w = 0; w < beam_width; ++w) RET_IF(kv_cache_reserve(d->kv, b0 + w, ctx_len));
   }
   RET_IF(kv_cache_sync(d->kv, d->stream));
-  const size_t n = (size_t)k->num_pages * k->page_elems;
-  LLM_HIP_RET(launch_fill_random_f16(k->k_pool, n, seed * 2 + 1, 0.05f, d->stream));
-  LLM_HIP_RET(launch_fill_random_f16(k->v_pool, n, seed * 2 + 2, 1.0f, d->stream));
+  const size_t np = (size_t)k->num_pages, pe = k->page_elems, ps = k->page_stride() / k->es;
+  LLM_HIP_RET(launch_fill_random_f16(k->k_pool, np, pe, ps, seed * 2 + 1, 0.05f, d->stream));
+  LLM_HIP_RET(launch_fill_random_f16(k->v_pool, np, pe, ps, seed * 2 + 2, 1.0f, d->stream));
   LLM_HIP_RET(hipStreamSynchronize(d->stream));
   d->row_group = beam_width;
   d->graph_batch = -1;  // re-capture: the attention launch depends on row_group

@@ -38,6 +38,7 @@ struct KvAppend {
   _Float16* k_pool;
   _Float16* v_pool;
   int num_beams, max_tiles, TS, num_pages, H, D;
+  size_t page_stride;  // elements from page p to page p + 1
 };
 
 struct GemmArgs {
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       const int i = n - hid * (1 + which);
       const int d = i % kv.D;
       const int p = e_pos[e];
-      const size_t off = ((size_t)e_page[e] * kv.TS + (p % kv.TS)) * kv.D + d;
+      const size_t off = (size_t)e_page[e] * kv.page_stride + (size_t)(p % kv.TS) * kv.D + d;
       (which ? kv.v_pool : kv.k_pool)[off] = (_Float16)y;
     }
   }
@@ -507,7 +508,8 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");
     a.kv = KvAppend{kv.pos, kv.page_table, kv.rows, static_cast<_Float16*>(kv.k_pool),
                     static_cast<_Float16*>(kv.v_pool), kv.num_beams, kv.max_tiles, kv.page_size,
-                    kv.num_pages, kv.H, kv.D};
+                    kv.num_pages, kv.H, kv.D,
+                    kv.page_stride > 0 ? kv.page_stride : (size_t)kv.page_size * kv.D};
   }
   const hipError_t e = g.dtype == LLM_I8 ? launch_gemm<GemmKind::I8>(a, st)
                                          : launch_gemm<GemmKind::F16>(a, st);

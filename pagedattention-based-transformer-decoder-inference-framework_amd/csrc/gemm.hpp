@@ -18,6 +18,7 @@ struct KvAppendView {
   void* k_pool;
   void* v_pool;
   int num_beams = 0, max_tiles = 0, page_size = 0, num_pages = 0, H = 0, D = 0;
+  size_t page_stride = 0;  // fp16 elements from page p to page p + 1 (0: one page)
 };
 
 // One decode weight GEMM (decoder-internal form of i8_gemm / f16_gemm):

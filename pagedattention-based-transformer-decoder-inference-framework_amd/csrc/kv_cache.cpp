@@ -13,8 +13,10 @@
 //     page id = map.size() aliases live pages after an eviction,
 //     kv_tile_cache.cpp:71), so beams can fork and share prefix pages;
 //   * copy-on-write of a shared page before a token is written into it.
-// Pools are one hipMalloc each ([num_pages][page_size][head_dim] fp16), sized
-// for the 288 GB HBM of an MI355X (page ids are int32, byte offsets 64-bit).
+// The K and V pools interleave page by page in ONE hipMalloc:
+// [num_pages][K page | V page], so page p's K and V are adjacent (see
+// KvCache::init), sized for the 288 GB HBM of an MI355X (page ids are int32,
+// byte offsets 64-bit).
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -34,7 +36,7 @@ template <typename E>
 __global__ void kv_write_tokens_kernel(const E* __restrict__ ksrc, const E* __restrict__ vsrc,
                                        int n, int H, int D, int pos0, int beam,
                                        const int32_t* __restrict__ table, int max_tiles, int TS,
-                                       long long num_pages, E* __restrict__ kp,
+                                       long long num_pages, size_t page_stride, E* __restrict__ kp,
                                        E* __restrict__ vp) {
   const size_t total = (size_t)n * H * D;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -47,7 +49,7 @@ __global__ void kv_write_tokens_kernel(const E* __restrict__ ksrc, const E* __re
     if (tile >= max_tiles) continue;
     const int page = table[((size_t)beam * H + h) * max_tiles + tile];
     if (page < 0 || page >= num_pages) continue;
-    const size_t off = ((size_t)page * TS + pos % TS) * D + d;
+    const size_t off = (size_t)page * page_stride + (size_t)(pos % TS) * D + d;
     kp[off] = ksrc[i];
     vp[off] = vsrc[i];
   }
@@ -59,12 +61,19 @@ int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, l
   dtype = dtype_;
   es = dtype == LLM_F32 ? 4 : dtype == LLM_I8 ? 1 : 2;
   page_elems = (size_t)TS * D;
-  const size_t pool_bytes = (size_t)num_pages * page_bytes();
-  if (hipMalloc(&k_pool, pool_bytes) != hipSuccess || hipMalloc(&v_pool, pool_bytes) != hipSuccess) {
+  // A wave loads K page p and V page p together.  With two separate pools at
+  // a large distance the pair often falls into the same HBM channel and the
+  // scan loses 2-4 %, depending on the distance (C3 shape,
+  // scripts/tune_attention.py --v-gap: 648-685 us across V-pool offsets);
+  // adjacent K / V pages measured 649 us at every context length tried
+  // (--interleave).
+  const size_t alloc = (size_t)num_pages * page_stride();
+  if (hipMalloc(&k_pool, alloc) != hipSuccess) {
     (void)hipGetLastError();
-    return fail(LLM_ERR_OOM, "kv_cache: cannot allocate " + std::to_string(2 * pool_bytes) +
+    return fail(LLM_ERR_OOM, "kv_cache: cannot allocate " + std::to_string(alloc) +
                                  " bytes of page pool");
   }
+  v_pool = static_cast<char*>(k_pool) + page_bytes();
   entries = (size_t)L * beams * H * max_tiles;
   LLM_HIP_RET(hipMalloc(&d_table, entries * sizeof(int32_t)));
   LLM_HIP_RET(hipMemset(d_table, 0xFF, entries * sizeof(int32_t)));  // -1 (page_table.cpp:22-25)
@@ -79,8 +88,7 @@ int KvCache::init(int L_, int beams_, int H_, int D_, int TS_, int max_tiles_, l
 
 KvCache::~KvCache() {
   if (staging_done) (void)hipEventSynchronize(staging_done);
-  if (k_pool) (void)hipFree(k_pool);
-  if (v_pool) (void)hipFree(v_pool);
+  if (k_pool) (void)hipFree(k_pool);  // v_pool lives in the same allocation
   if (d_table) (void)hipFree(d_table);
   if (d_idx) (void)hipFree(d_idx);
   if (d_val) (void)hipFree(d_val);
@@ -182,14 +190,12 @@ int KvCache::prepare_append(int beam, int pos) {
 }
 
 int KvCache::sync(hipStream_t st) {
-  // pending copy-on-write page copies first (old page -> new page, K and V)
+  // pending copy-on-write page copies first (old page -> new page; K and V
+  // are adjacent, one copy each)
   for (const auto& c : cow) {
-    const size_t bytes = page_bytes();
+    const size_t bytes = page_stride();
     LLM_HIP_RET(hipMemcpyAsync((char*)k_pool + (size_t)c.second * bytes,
                                (char*)k_pool + (size_t)c.first * bytes, bytes,
-                               hipMemcpyDeviceToDevice, st));
-    LLM_HIP_RET(hipMemcpyAsync((char*)v_pool + (size_t)c.second * bytes,
-                               (char*)v_pool + (size_t)c.first * bytes, bytes,
                                hipMemcpyDeviceToDevice, st));
   }
   cow.clear();
@@ -278,6 +284,7 @@ extern "C" int kv_cache_view(const kv_cache* c, int layer, pa_kv_view* out) {
   out->page_size = k.TS;
   out->head_dim = k.D;
   out->num_beams = k.beams;
+  out->page_stride = (int64_t)k.page_stride();
   out->num_heads = k.H;
   out->max_tiles = k.max_tiles;
   out->kv_dtype = k.dtype;
@@ -441,8 +448,8 @@ extern "C" int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, 
     using E = decltype(tag);
     hipLaunchKernelGGL(kv_write_tokens_kernel<E>, grid, dim3(256), 0, nullptr,
                        static_cast<const E*>(dk), static_cast<const E*>(dv), n, k.H, k.D, pos,
-                       beam, table, k.max_tiles, k.TS, k.num_pages, static_cast<E*>(k.k_pool),
-                       static_cast<E*>(k.v_pool));
+                       beam, table, k.max_tiles, k.TS, k.num_pages, k.page_stride() / k.es,
+                       static_cast<E*>(k.k_pool), static_cast<E*>(k.v_pool));
   };
   if (k.es == 4) launch(uint32_t{});
   else if (k.es == 1) launch(uint8_t{});
@@ -456,6 +463,9 @@ extern "C" int kv_cache_write_tokens(kv_cache* c, int layer, int beam, int pos, 
 
 extern "C" void* kv_cache_k_pool(kv_cache* c) { return c ? c->impl.k_pool : nullptr; }
 extern "C" void* kv_cache_v_pool(kv_cache* c) { return c ? c->impl.v_pool : nullptr; }
+extern "C" long long kv_cache_page_stride(const kv_cache* c) {
+  return c ? (long long)c->impl.page_stride() : 0;
+}
 extern "C" int32_t* kv_cache_page_table(kv_cache* c, int layer) {
   if (!c || layer < 0 || layer >= c->impl.L) return nullptr;
   const KvCache& k = c->impl;
@@ -487,9 +497,12 @@ extern "C" int kv_cache_save(const kv_cache* c, const char* path) {
   std::vector<char> buf(pb);
   LLM_HIP_RET(hipDeviceSynchronize());
   for (int32_t p : used) {
-    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.k_pool + (size_t)p * pb, pb, hipMemcpyDeviceToHost));
+    // file order per page: K then V (the pool's own page order)
+    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.k_pool + (size_t)p * k.page_stride(), pb,
+                          hipMemcpyDeviceToHost));
     f.write(buf.data(), pb);
-    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.v_pool + (size_t)p * pb, pb, hipMemcpyDeviceToHost));
+    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.v_pool + (size_t)p * k.page_stride(), pb,
+                          hipMemcpyDeviceToHost));
     f.write(buf.data(), pb);
   }
   if (!f) return fail(LLM_ERR_IO, "kv_cache_save: write failed");
@@ -526,9 +539,11 @@ extern "C" int kv_cache_load(kv_cache* c, const char* path) {
   std::vector<char> buf(pb);
   for (int32_t p : used) {
     f.read(buf.data(), pb);
-    LLM_HIP_RET(hipMemcpy((char*)k.k_pool + (size_t)p * pb, buf.data(), pb, hipMemcpyHostToDevice));
+    LLM_HIP_RET(hipMemcpy((char*)k.k_pool + (size_t)p * k.page_stride(), buf.data(), pb,
+                          hipMemcpyHostToDevice));
     f.read(buf.data(), pb);
-    LLM_HIP_RET(hipMemcpy((char*)k.v_pool + (size_t)p * pb, buf.data(), pb, hipMemcpyHostToDevice));
+    LLM_HIP_RET(hipMemcpy((char*)k.v_pool + (size_t)p * k.page_stride(), buf.data(), pb,
+                          hipMemcpyHostToDevice));
   }
   if (!f) return fail(LLM_ERR_IO, "kv_cache_load: truncated page data");
   // rebuild refcounts / free list from the table

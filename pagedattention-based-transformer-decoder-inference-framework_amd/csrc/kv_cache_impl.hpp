@@ -20,8 +20,8 @@ struct KvCache {
   int es = 2;           // bytes per element
   size_t page_elems = 0;
   size_t entries = 0;
-  void* k_pool = nullptr;
-  void* v_pool = nullptr;
+  void* k_pool = nullptr;  // page p of K at k_pool + p * page_stride(), V right after it
+  void* v_pool = nullptr;  // = k_pool + page_bytes() (same allocation)
   int32_t* d_table = nullptr;
   std::vector<int32_t> h_table;     // host mirror = source of truth
   std::vector<uint8_t> dirty_flag;
@@ -47,6 +47,7 @@ struct KvCache {
   int init(int L, int beams, int H, int D, int TS, int max_tiles, long long pages,
            int dtype = LLM_F16);
   size_t page_bytes() const { return page_elems * es; }
+  size_t page_stride() const { return 2 * page_bytes(); }  // K and V pages interleave
   size_t index(int layer, int beam, int head, int tile) const {
     return (((size_t)layer * beams + beam) * H + head) * max_tiles + tile;
   }

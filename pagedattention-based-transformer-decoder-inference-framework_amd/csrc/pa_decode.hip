@@ -58,6 +58,7 @@ struct PaSplitArgs {
   const int32_t* context_lens;
   int B, H, T;
   int num_pages, num_beams, max_tiles;
+  size_t page_stride;  // bytes from page p to page p + 1 (K and V pages may interleave)
   int pps;     // > 0: fixed pages per split (<= 128); 0: ceil(ntiles_b / nsplit)
   int nsplit;  // splits per (b, h) (grid)
   int group;   // rows per wave group (beam width): the group's rows for one (head, split)
@@ -232,7 +233,7 @@ void pa_split_kernel(PaSplitArgs a) {
       const int j = p0 + u;
       const int pg = page_of(min(j, kMaxPps - 1));
       const bool ok = (j < count) && (pg >= 0);
-      const size_t off = (size_t)(ok ? pg : 0) * PAGE_BYTES;
+      const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
       const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k_pool + off), (short)0,
                                                          ok ? PAGE_BYTES : 0, 0x00020000);
       const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.v_pool + off), (short)0,
@@ -330,7 +331,7 @@ void pa_split_kernel(PaSplitArgs a) {
           const int j = cc * U + u;
           const int pg = page_of(min(j, kMaxPps - 1));
           const bool ok = (j < count) && (pg >= 0);
-          const size_t off = (size_t)(ok ? pg : 0) * PAGE_BYTES;
+          const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
           const uint8_t* pool = q < NR ? a.k_pool : a.v_pool;
           const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pool + off), (short)0,
                                                             ok ? PAGE_BYTES : 0, 0x00020000);
@@ -788,8 +789,11 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     return fail(LLM_ERR_UNSUPPORTED, "pa_decode: unsupported head_dim/page_size/kv_dtype (D in "
                                      "{32,64,128,256}, page_size in {16,32}, one page of "
                                      "1..16 KiB)");
-  LLM_REQUIRE((long long)kv->num_pages * kv->page_size * D * kv_dtype_bytes(kv->kv_dtype) <
-                  (1LL << 47),
+  const size_t page_stride = kv_view_page_stride(*kv);
+  LLM_REQUIRE(page_stride >= (size_t)kv->page_size * D * kv_dtype_bytes(kv->kv_dtype) &&
+                  page_stride % 16 == 0,
+              "pa_decode: page_stride must be 0 or >= one page and a multiple of 16");
+  LLM_REQUIRE((long long)kv->num_pages * (long long)page_stride < (1LL << 47),
               "pa_decode: pool too large");
   const int TS = kv->page_size;
   // tiles at or past max_tiles have no page-table entry: they are missing (masked)
@@ -830,6 +834,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   a.num_pages = kv->num_pages;
   a.num_beams = kv->num_beams;
   a.max_tiles = kv->max_tiles;
+  a.page_stride = page_stride;
   a.pps = pps_fixed;
   a.nsplit = nsplit;
   a.group = std::max(1, std::min(row_group, 4));
@@ -915,6 +920,7 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
   a.context_lens = context_lens;
   a.B = B; a.H = H; a.T = T;
   a.num_pages = kv->num_pages; a.num_beams = kv->num_beams; a.max_tiles = kv->max_tiles;
+  a.page_stride = kv_view_page_stride(*kv);
   a.pps = pps; a.nsplit = nsplit; a.group = 1; a.qscale = kLog2e;
   a.part_acc = static_cast<float*>(workspace);
   a.part_ml = a.part_acc + (size_t)B * H * nsplit * 128;

@@ -27,4 +27,15 @@ int pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float
                        int waves_per_simd = 0);
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 
+// Bytes per element of a KV pool type (0: unknown type).
+inline int kv_elem_size(int kvt) {
+  return kvt == LLM_F16 || kvt == LLM_BF16 ? 2 : kvt == LLM_F32 ? 4 : kvt == LLM_I8 ? 1 : 0;
+}
+
+// Bytes from page p to page p + 1 of a view's pools (page_stride 0 = dense).
+inline size_t kv_view_page_stride(const pa_kv_view& v) {
+  return v.page_stride > 0 ? (size_t)v.page_stride
+                           : (size_t)v.page_size * v.head_dim * kv_elem_size(v.kv_dtype);
+}
+
 }  // namespace llm

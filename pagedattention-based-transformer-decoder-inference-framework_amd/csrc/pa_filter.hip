@@ -19,6 +19,9 @@
 // apply_topk_topp_filter sorts by (attention_cpu/softmax_lut.cpp:233-256),
 // ties broken toward the larger index.
 #include "common.hpp"
+#include "pa_decode.hpp"
+
+#include <algorithm>
 
 #include <string>
 
@@ -39,6 +42,7 @@ struct PaFilterArgs {
   const int32_t* context_lens;
   int B, H, D, T, TS;
   int num_pages, num_beams, max_tiles;
+  size_t page_stride;  // elements from page p to page p + 1
   float temperature;
   int top_k;
   float top_p;
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(kFilterThreads) void pa_filter_kernel(PaFilterArgs 
     const int p = page_of(t);
     float s = -1e9f;
     if (p >= 0) {
-      const size_t base = ((size_t)p * a.TS + t % a.TS) * D;
+      const size_t base = (size_t)p * a.page_stride + (size_t)(t % a.TS) * D;
       float dot = 0.f;
       for (int d = 0; d < D; ++d) dot += qs[d] * kv_elem<KVT>(a.k_pool, base + d);
       s = dot / a.temperature;
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(kFilterThreads) void pa_filter_kernel(PaFilterArgs 
       if (p == 0.f) continue;
       const int pg = page_of(t);
       if (pg < 0) continue;
-      acc += p * kv_elem<KVT>(a.v_pool, ((size_t)pg * a.TS + t % a.TS) * D + d);
+      acc += p * kv_elem<KVT>(a.v_pool, (size_t)pg * a.page_stride + (size_t)(t % a.TS) * D + d);
     }
   float* red = reinterpret_cast<float*>(key);
   __syncthreads();
@@ -244,6 +248,11 @@ extern "C" int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out,
   LLM_REQUIRE(kv->page_size > 0 && kv->num_pages > 0 && kv->num_beams > 0 && kv->max_tiles > 0,
               "pa_decode_ex: empty kv view");
   LLM_REQUIRE(opt->top_p > 0.f, "pa_decode_ex: top_p must be > 0");
+  LLM_REQUIRE(kv->page_stride == 0 ||
+                  (kv->page_stride >= (int64_t)kv->page_size * kv->head_dim *
+                                          kv_elem_size(kv->kv_dtype) &&
+                   kv->page_stride % 16 == 0),
+              "pa_decode_ex: page_stride must be 0 or >= one page and a multiple of 16");
   if (T > kFilterMaxT || D > 256)
     return fail(LLM_ERR_UNSUPPORTED, "pa_decode_ex: filters / weight outputs need T <= 8192 and "
                                      "D <= 256");
@@ -259,6 +268,7 @@ extern "C" int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out,
   a.context_lens = context_lens;
   a.B = B; a.H = H; a.D = D; a.T = T; a.TS = kv->page_size;
   a.num_pages = kv->num_pages; a.num_beams = kv->num_beams; a.max_tiles = kv->max_tiles;
+  a.page_stride = kv_view_page_stride(*kv) / std::max(1, kv_elem_size(kv->kv_dtype));
   a.temperature = opt->temperature;
   a.top_k = opt->top_k;
   a.top_p = opt->top_p;

@@ -298,29 +298,6 @@ __global__ __launch_bounds__(kRowThreads) void embed_kernel(const _Float16* __re
   for (int i = threadIdx.x; i < hid; i += blockDim.x) xr[i] = (float)e[i];
 }
 
-// Append this step's K and V (fp32 rows of the qkv projection, layout
-// [b][q|k|v][H][D]) into the pages of position pos[b]
-// (KVTileCache::get_write_ptr, kv_cache/kv_tile_cache.hpp:28-34).
-__global__ __launch_bounds__(kRowThreads) void kv_append_kernel(
-    const float* __restrict__ qkv, int H, int D, const int32_t* __restrict__ pos,
-    const int32_t* __restrict__ page_table, int num_beams, int max_tiles, int TS, int num_pages,
-    _Float16* __restrict__ k_pool, _Float16* __restrict__ v_pool) {
-  const int b = blockIdx.x;
-  const int hid = H * D;
-  const int p = pos[b];
-  const int tile = p / TS, row = p % TS;
-  const float* src = qkv + (size_t)b * 3 * hid;
-  for (int i = threadIdx.x; i < hid; i += blockDim.x) {
-    const int h = i / D, d = i % D;
-    if (b >= num_beams || tile >= max_tiles) continue;
-    const int page = page_table[((size_t)b * H + h) * max_tiles + tile];
-    if (page < 0 || page >= num_pages) continue;
-    const size_t off = ((size_t)page * TS + row) * D + d;
-    k_pool[off] = (_Float16)src[hid + i];
-    v_pool[off] = (_Float16)src[2 * hid + i];
-  }
-}
-
 // pack_cols > 0: y is packed-A fp16 of rows of pack_cols (x row-major [n / pack_cols][pack_cols]).
 __global__ void to_f16_kernel(const float* __restrict__ x, size_t n, _Float16* __restrict__ y,
                               int pack_cols) {
@@ -352,8 +329,11 @@ __global__ void scatter_i32_kernel(int32_t* __restrict__ dst, const int64_t* __r
 
 // Seeded random fp16 fill (synthetic KV contexts): splitmix64 -> ~N(0,1)*scale
 // via the sum of 4 uniforms (Irwin-Hall), cheap and deterministic.
-__global__ void fill_random_f16_kernel(_Float16* __restrict__ p, size_t n, uint64_t seed,
-                                       float scale) {
+// Element i of the n = pages * page_elems lands at p[(i / page_elems) *
+// page_stride + i % page_elems] (page_stride in elements: a pool whose pages
+// interleave with another pool's).
+__global__ void fill_random_f16_kernel(_Float16* __restrict__ p, size_t n, size_t page_elems,
+                                       size_t page_stride, uint64_t seed, float scale) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (; i < n; i += stride) {
@@ -364,7 +344,7 @@ __global__ void fill_random_f16_kernel(_Float16* __restrict__ p, size_t n, uint6
     float u = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) u += (float)((z >> (16 * k)) & 0xFFFF) * (1.0f / 65536.0f);
-    p[i] = (_Float16)((u - 2.0f) * 1.7320508f * scale);
+    p[(i / page_elems) * page_stride + i % page_elems] = (_Float16)((u - 2.0f) * 1.7320508f * scale);
   }
 }
 
@@ -449,15 +429,6 @@ hipError_t launch_embed(const void* E, const int32_t* tok, int rows, int hid, in
   return hipGetLastError();
 }
 
-hipError_t launch_kv_append(const float* qkv, int rows, int H, int D, const int32_t* pos,
-                            const int32_t* page_table, int num_beams, int max_tiles, int TS,
-                            int num_pages, void* k_pool, void* v_pool, hipStream_t st) {
-  hipLaunchKernelGGL(kv_append_kernel, dim3(rows), dim3(kRowThreads), 0, st, qkv, H, D, pos,
-                     page_table, num_beams, max_tiles, TS, num_pages,
-                     static_cast<_Float16*>(k_pool), static_cast<_Float16*>(v_pool));
-  return hipGetLastError();
-}
-
 hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* val, int n,
                               hipStream_t st) {
   if (n <= 0) return hipSuccess;
@@ -465,11 +436,13 @@ hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* v
   return hipGetLastError();
 }
 
-hipError_t launch_fill_random_f16(void* p, size_t n, uint64_t seed, float scale, hipStream_t st) {
+hipError_t launch_fill_random_f16(void* p, size_t pages, size_t page_elems, size_t page_stride,
+                                  uint64_t seed, float scale, hipStream_t st) {
+  const size_t n = pages * page_elems;
   if (n == 0) return hipSuccess;
   const size_t blocks = std::min<size_t>((n + 255) / 256, 65536);
   hipLaunchKernelGGL(fill_random_f16_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     static_cast<_Float16*>(p), n, seed, scale);
+                     static_cast<_Float16*>(p), n, page_elems, page_stride, seed, scale);
   return hipGetLastError();
 }
 

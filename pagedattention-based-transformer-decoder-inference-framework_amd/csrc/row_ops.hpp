@@ -24,9 +24,6 @@ hipError_t launch_argmax(const float* logits, int rows, int V, int32_t* out, int
                          int out2_stride, hipStream_t st);
 hipError_t launch_embed(const void* E, const int32_t* tok, int rows, int hid, int V, float* x,
                         hipStream_t st);
-hipError_t launch_kv_append(const float* qkv, int rows, int H, int D, const int32_t* pos,
-                            const int32_t* page_table, int num_beams, int max_tiles, int TS,
-                            int num_pages, void* k_pool, void* v_pool, hipStream_t st);
 hipError_t launch_scatter_i32(int32_t* dst, const int64_t* idx, const int32_t* val, int n,
                               hipStream_t st);
 // LM head (csrc/lm_head.hip): logits = x . E^T (E packed by launch_lm_pack); with part_val/part_idx also the
@@ -42,6 +39,9 @@ hipError_t launch_argmax_partials(const float* part_val, const int32_t* part_idx
 hipError_t launch_sample(const float* logits, int rows, int row0, int V, float temperature,
                          int top_k, float top_p, uint64_t seed, const int32_t* counter,
                          int32_t* out, hipStream_t st);
-hipError_t launch_fill_random_f16(void* p, size_t n, uint64_t seed, float scale, hipStream_t st);
+// Seeded uniform (variance-1 x scale) fp16 over `pages` pages of page_elems
+// elements, page p at p + p * page_stride elements.
+hipError_t launch_fill_random_f16(void* p, size_t pages, size_t page_elems, size_t page_stride,
+                                  uint64_t seed, float scale, hipStream_t st);
 
 }  // namespace llm

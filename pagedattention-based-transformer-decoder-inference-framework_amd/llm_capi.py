@@ -31,7 +31,7 @@ class PaKvView(ctypes.Structure):
                 ("num_pages", ctypes.c_int32), ("page_size", ctypes.c_int32),
                 ("head_dim", ctypes.c_int32), ("num_beams", ctypes.c_int32),
                 ("num_heads", ctypes.c_int32), ("max_tiles", ctypes.c_int32),
-                ("kv_dtype", ctypes.c_int32)]
+                ("kv_dtype", ctypes.c_int32), ("page_stride", ctypes.c_int64)]
 
 
 class PaDecodeOptions(ctypes.Structure):
@@ -96,6 +96,7 @@ _SIGS = {
     "kv_cache_write_tokens": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "kv_cache_k_pool": (c_void_p, [c_void_p]),
     "kv_cache_v_pool": (c_void_p, [c_void_p]),
+    "kv_cache_page_stride": (ctypes.c_longlong, [c_void_p]),
     "kv_cache_page_table": (c_void_p, [c_void_p, c_int]),
     "kv_cache_save": (c_int, [c_void_p, ctypes.c_char_p]),
     "kv_cache_load": (c_int, [c_void_p, ctypes.c_char_p]),
@@ -164,8 +165,16 @@ def kv_dtype_of(t) -> int:
 
 def kv_view(k_pool, v_pool, page_table, *, num_beams=None) -> PaKvView:
     """View over torch device tensors k/v [num_pages][ts][D] (fp16, bf16, fp32
-    or int8, both the same) and page table int32 [num_beams][H][max_tiles]."""
+    or int8, both the same) and page table int32 [num_beams][H][max_tiles].
+    Pages may be strided (e.g. k = kv[:, 0], v = kv[:, 1] of one
+    [num_pages][2][ts][D] tensor: K and V pages interleaved) as long as each
+    page is contiguous; the view's page_stride is then the page-to-page step."""
     nb, H, mt = page_table.shape
+    for t in (k_pool, v_pool):
+        if t.dim() != 3 or t.stride(2) != 1 or t.stride(1) != t.shape[2]:
+            raise ValueError("KV pools must be [num_pages][ts][D] with contiguous pages")
+    if k_pool.stride(0) != v_pool.stride(0):
+        raise ValueError("k_pool and v_pool must share one page stride")
     v = PaKvView()
     v.k_pool, v.v_pool, v.page_table = k_pool.data_ptr(), v_pool.data_ptr(), page_table.data_ptr()
     v.num_pages, v.page_size, v.head_dim = k_pool.shape[0], k_pool.shape[1], k_pool.shape[2]
@@ -173,6 +182,8 @@ def kv_view(k_pool, v_pool, page_table, *, num_beams=None) -> PaKvView:
     if k_pool.dtype != v_pool.dtype:
         raise TypeError("k_pool and v_pool must have the same dtype")
     v.kv_dtype = kv_dtype_of(k_pool)
+    dense = k_pool.shape[1] * k_pool.shape[2]
+    v.page_stride = 0 if k_pool.stride(0) == dense else k_pool.stride(0) * k_pool.element_size()
     return v
 
 

@@ -56,8 +56,8 @@ for s in range(NS):
         v = llm_capi.PaKvView()
         llm_capi.check(lib.kv_cache_view(h, l, ctypes.byref(v)))
         TS, D, H = v.page_size, v.head_dim, v.num_heads
-        kp = d2h(v.k_pool, v.num_pages * TS * D, np.float16).reshape(v.num_pages, TS, D)
-        vp = d2h(v.v_pool, v.num_pages * TS * D, np.float16).reshape(v.num_pages, TS, D)
+        both = d2h(v.k_pool, v.num_pages * 2 * TS * D, np.float16).reshape(v.num_pages, 2, TS, D)
+        kp, vp = both[:, 0], both[:, 1]  # K / V pages interleave
         pt = d2h(v.page_table, v.num_beams * H * v.max_tiles, np.int32).reshape(v.num_beams, H, v.max_tiles)
         ok = o_k = odec.kv(l, 0)
         o_v = odec.kv(l, 1)

@@ -48,8 +48,8 @@ hnd = ctypes.c_void_p(dec.kv_handle)
 v = llm_capi.PaKvView()
 llm_capi.check(lib.kv_cache_view(hnd, 0, ctypes.byref(v)))
 TS = v.page_size
-kp = d2h(v.k_pool, v.num_pages * TS * D, np.float16).reshape(v.num_pages, TS, D)
-vp = d2h(v.v_pool, v.num_pages * TS * D, np.float16).reshape(v.num_pages, TS, D)
+both = d2h(v.k_pool, v.num_pages * 2 * TS * D, np.float16).reshape(v.num_pages, 2, TS, D)
+kp, vp = both[:, 0], both[:, 1]  # K / V pages interleave
 pt = d2h(v.page_table, v.num_beams * H * v.max_tiles, np.int32).reshape(v.num_beams, H, v.max_tiles)
 
 dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()

@@ -28,11 +28,16 @@ ap.add_argument("--interleave", action="store_true",
 ap.add_argument("--extent", type=int, default=1,
                 help="tiles per physically contiguous page run (1 = fully random pages; "
                      "nt = each (row, head) contiguous)")
+ap.add_argument("--pool-pages", type=int, default=0,
+                help="pages in each pool (>= B*H*tiles; the used pages are a random subset)")
+ap.add_argument("--seed", type=int, default=0)
+ap.add_argument("--v-gap", type=int, default=-1,
+                help=">= 0: K and V pools in ONE allocation, V starting this many pages after K's end")
 args = ap.parse_args()
 B, H, D, T, ts = args.B, 16, 128, args.T, 16
 nt = (T + ts - 1) // ts
-num_pages = B * H * nt
-g = torch.Generator(device="cuda").manual_seed(0)
+num_pages = max(B * H * nt, args.pool_pages)
+g = torch.Generator(device="cuda").manual_seed(args.seed)
 if args.interleave:
     kv = torch.randn((2 * num_pages, ts, D), generator=g, device="cuda").half()
     kp, vp = kv[:-1], kv[1:]  # page p of kp = kv[p], of vp = kv[p + 1]
@@ -41,8 +46,14 @@ if args.interleave:
 else:
     kp = (torch.randn((num_pages, ts, D), generator=g, device="cuda") * D ** -0.25).half()
     vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
+    if args.v_gap >= 0:
+        both = torch.empty((2 * num_pages + args.v_gap, ts, D), device="cuda", dtype=torch.half)
+        both[:num_pages] = kp
+        both[num_pages + args.v_gap:] = vp
+        del kp, vp
+        kp, vp = both[:num_pages], both[num_pages + args.v_gap:]
     q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
-    pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
+    pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32)[:B * H * nt].reshape(B, H, nt)
 if args.extent > 1 and not args.interleave:
     ext = args.extent
     assert nt % ext == 0

@@ -105,8 +105,11 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
         assert hip.hipMemcpy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(ptr),
                              n * t.element_size(), 3) == 0
         return t
-    kpool = dev_copy(view["k_pool"], num_pages * TS * D, torch.float16).reshape(num_pages, TS, D)
-    vpool = dev_copy(view["v_pool"], num_pages * TS * D, torch.float16).reshape(num_pages, TS, D)
+    # K and V pages interleave in one allocation: [num_pages][K page | V page]
+    assert view["page_stride"] == 2 * TS * D * 2
+    assert view["v_pool"] == view["k_pool"] + TS * D * 2
+    both = dev_copy(view["k_pool"], num_pages * 2 * TS * D, torch.float16).reshape(num_pages, 2, TS, D)
+    kpool, vpool = both[:, 0], both[:, 1]
     table = dev_copy(view["page_table"], beams * H * 8, torch.int32).reshape(beams, H, 8)
     # the pools hold exactly what was written, per beam
     for b in range(beams):
@@ -139,7 +142,8 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
         for t in range(4):
             assert kv2.lookup(b, 0, t) == kv.lookup(b, 0, t)
     v2 = kv2.view(0)
-    kpool2 = dev_copy(v2["k_pool"], num_pages * TS * D, torch.float16).reshape(num_pages, TS, D)
+    kpool2 = dev_copy(v2["k_pool"], num_pages * 2 * TS * D,
+                      torch.float16).reshape(num_pages, 2, TS, D)[:, 0]
     used = sorted({kv.lookup(b, h, t) for b in range(beams) for h in range(H) for t in range(4)})
     # bitwise (rows past the written tokens are never-written bits, possibly NaN)
     assert torch.equal(kpool2[used].view(torch.int16), kpool[used].view(torch.int16))

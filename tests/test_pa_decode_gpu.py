@@ -259,6 +259,46 @@ def test_pa_decode_kv_dtypes_vs_oracle(gpu, oracle, kv_dtype, B, H, D, T, ts):
         assert rel_err(out, ref) < RTOL, (kv_dtype, pps, rel_err(out, ref))
 
 
+@pytest.mark.parametrize("kv_dtype", ["float16", "bfloat16", "float32", "int8"])
+def test_pa_decode_interleaved_pools_bitwise(gpu, oracle, kv_dtype):
+    """Pools whose K and V pages interleave in one allocation
+    ([num_pages][K page | V page], the kv_cache layout; pa_kv_view.page_stride
+    = 2 pages) give bit-identical outputs to dense copies of the same pools,
+    on the split kernel (one and several splits), the beam-aware schedule and
+    the filter path (pa_decode_ex)."""
+    import torch
+    import llm_capi
+    dt = getattr(torch, kv_dtype)
+    B, H, D, T, ts = 4, 3, 128, 700, 16
+    rng = np.random.default_rng(11)
+    nt = (T + ts - 1) // ts
+    num_pages = B * H * nt + 5
+    qs = 0.1 if dt == torch.int8 else D ** -0.25
+    q = _dev((rng.standard_normal((B, H, D)) * qs).astype(np.float32))
+    kd, kf = _kv_elems(rng, dt, (num_pages, ts, D), D ** -0.25)
+    vd, vf = _kv_elems(rng, dt, (num_pages, ts, D), 1.0)
+    both = torch.stack([kd, vd], dim=1).contiguous()  # [P][2][ts][D]
+    ki, vi = both[:, 0], both[:, 1]
+    assert llm_capi.kv_view(ki, vi, _dev(np.zeros((1, H, nt), np.int32))).page_stride == \
+        2 * ts * D * both.element_size()
+    pt = _dev(rng.permutation(num_pages)[: B * H * nt].astype(np.int32).reshape(B, H, nt))
+    lens = _dev(rng.integers(1, T + 1, size=B).astype(np.int32))
+    ref = oracle.paged_attention(q.cpu().numpy(), kf, vf, pt.cpu().numpy(), T=T,
+                                 context_lens=lens.cpu().numpy())
+    for pps in (0, 4, 64):
+        dense = llm_capi.pa_decode(q, kd, vd, pt, T=T, context_lens=lens, pages_per_split=pps)
+        inter = llm_capi.pa_decode(q, ki, vi, pt, T=T, context_lens=lens, pages_per_split=pps)
+        assert torch.equal(dense, inter), (kv_dtype, pps)
+        assert rel_err(inter.cpu().numpy(), ref) < RTOL
+    if dt == torch.float16:  # beam-aware prefetch form (fp16 pools, groups of 4)
+        dense = llm_capi.pa_decode(q, kd, vd, pt, T=T, context_lens=lens, row_group=4)
+        inter = llm_capi.pa_decode(q, ki, vi, pt, T=T, context_lens=lens, row_group=4)
+        assert torch.equal(dense, inter)
+    dense = llm_capi.pa_decode_ex(q, kd, vd, pt, T=T, context_lens=lens, top_k=5)
+    inter = llm_capi.pa_decode_ex(q, ki, vi, pt, T=T, context_lens=lens, top_k=5)
+    assert torch.equal(dense, inter)
+
+
 FILTER_CASES = ["topk5", "topp09", "eos", "c1_base", "c1_missing", "beam_route", "temp07",
                 "ragged_tail", "ts32", "all_missing"]
 
