@@ -7,7 +7,8 @@ config shape a fixed number of times, for rocprofv3 kernel-trace / PMC passes:
         python3 scripts/prof_attention.py --config c3 --iters 20
 
 KV pools hold seeded random fp16 and pages are a shuffled permutation of the
-pool, so the gather is non-contiguous.
+pool, so the gather is non-contiguous; K and V pages interleave
+as in the decoder's kv_cache.
 """
 import argparse
 import ctypes
@@ -34,8 +35,10 @@ B, H, D, T, ts = c["B"], c["H"], c["D"], c["T"], c["ts"]
 nt = (T + ts - 1) // ts
 num_pages = B * H * nt
 g = torch.Generator(device="cuda").manual_seed(0)
-kp = (torch.randn((num_pages, ts, D), generator=g, device="cuda") * D ** -0.25).half()
-vp = torch.randn((num_pages, ts, D), generator=g, device="cuda").half()
+# the kv_cache layout: K and V pages interleave ([num_pages][K page | V page])
+kv = torch.randn((num_pages, 2, ts, D), generator=g, device="cuda").half()
+kv[:, 0] *= D ** -0.25
+kp, vp = kv[:, 0], kv[:, 1]
 q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
 pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
 out = torch.empty((B, H, D), device="cuda")
