@@ -498,6 +498,13 @@ struct PaMergeRowArgs {
   int pack;  // q / out16 in packed-A order (common.hpp a_frag_off_*)
 };
 
+// DPL = output dims per lane (D / 64, at least 1).  A head's split weights
+// (m, l) and the partials of its first kMergeBatch splits are loaded together,
+// so a merge costs one memory round trip (splits beyond the batch: one more
+// per batch); summation order s = 0, 1, ... as pa_merge_kernel.
+constexpr int kMergeBatch = 8;
+
+template <int DPL>
 __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   extern __shared__ float row[];  // [H*D]
   __shared__ float sh[16];
@@ -514,11 +521,21 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   for (int h = w; h < a.H; h += nw) {
     const size_t bh = (size_t)b * a.H + h;
     const float* ml = a.part_ml + bh * a.nsplit * 2;
+    const float* pa = a.part_acc + bh * a.nsplit * a.D;
     // split weights, lane-parallel: lane holds splits lane and 64 + lane
     const float m0 = lane < ns ? ml[2 * lane] : kNegSentinel;
     const float m1 = 64 + lane < ns ? ml[2 * (64 + lane)] : kNegSentinel;
     const float l0 = lane < ns ? ml[2 * lane + 1] : 0.f;
     const float l1 = 64 + lane < ns ? ml[2 * (64 + lane) + 1] : 0.f;
+    float v[kMergeBatch][DPL];
+#pragma unroll
+    for (int s2 = 0; s2 < kMergeBatch; ++s2)
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) {
+        const int d = lane + 64 * j;
+        // unconditional loads (clamped in range) so all issue before the first wait
+        v[s2][j] = pa[(size_t)min(s2, max(ns - 1, 0)) * a.D + min(d, a.D - 1)];
+      }
     const float M = wave_max(fmaxf(m0, m1));
     float* dst = row + h * a.D;
     if (ns <= 0 || M <= 0.5f * kNegSentinel) {
@@ -535,8 +552,37 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
       L += ls * ws;
     }
     const float inv = 1.0f / (L + 1e-6f);
-    const float* pa = a.part_acc + bh * a.nsplit * a.D;
-    for (int d = lane; d < a.D; d += 64) dst[d] = merge_splits(pa + d, a.D, ns, w0, w1) * inv;
+    float acc[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < kMergeBatch; ++s2) {
+      const float ws = __shfl(w0, s2, 64);  // 0 for s2 >= ns
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) acc[j] += v[s2][j] * ws;
+    }
+    for (int s0 = kMergeBatch; s0 < ns; s0 += 8) {  // long splits lists (rare)
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) {
+        const int d = lane + 64 * j;
+        float u[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[k] = (s0 + k < ns && d < a.D) ? pa[(size_t)(s0 + k) * a.D + d] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int s2 = s0 + k;
+          if (s2 < ns) {
+            const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
+            acc[j] += u[k] * ws;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) {
+      const int d = lane + 64 * j;
+      if (d < a.D) dst[d] = acc[j] * inv;
+    }
   }
   __syncthreads();
   float am = 0.f;
@@ -859,8 +905,13 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                       static_cast<_Float16*>(rows->out16), context_lens, B, H, D, T, TS, pps_fixed,
                       nsplit, kv->max_tiles, rows->pack};
     const int threads = 64 * std::min(16, H);  // one wave per head (heads > 16 loop)
-    hipLaunchKernelGGL(pa_merge_row_kernel, dim3(B), dim3(threads), (size_t)H * D * sizeof(float),
-                       st, mg);
+    const size_t lds = (size_t)H * D * sizeof(float);
+    if (D <= 64)
+      hipLaunchKernelGGL(pa_merge_row_kernel<1>, dim3(B), dim3(threads), lds, st, mg);
+    else if (D <= 128)
+      hipLaunchKernelGGL(pa_merge_row_kernel<2>, dim3(B), dim3(threads), lds, st, mg);
+    else
+      hipLaunchKernelGGL(pa_merge_row_kernel<4>, dim3(B), dim3(threads), lds, st, mg);
     LLM_HIP_RET(hipGetLastError());
     return LLM_OK;
   }

@@ -14,6 +14,6 @@ for line in sys.stdin:
         if cur: print(cur)
         cur = v[:70]
     else:
-        cur += f"  {k.split()[0]}{\"Spill\" if \"Spill\" in k else \"\"}={v}"
+        cur += "  " + k.split()[0] + ("Spill" if "Spill" in k else "") + "=" + v
 print(cur)
 '
