@@ -106,6 +106,20 @@ int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* out, const in
                       int pages_per_split, int row_group, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* Causal paged attention of a prompt chunk: the reference's prefill pass
+ * (AttentionCUDA's is_prefill flag, attention/attention_cuda.hpp:21; maths of
+ * cpu_paged_attention_forward, attention_cpu/cpu_attention_kernel.cpp:37-129,
+ * per query).  m query tokens of ONE sequence at positions p0 .. p0+m-1, whose
+ * K/V are already in the pages of page-table row `row`; query i attends to
+ * positions 0 .. p0+i.  Equals pa_decode with B = m, beam_ids[i] = row,
+ * context_lens[i] = p0 + i + 1 (within 1e-3 relative), but each K/V page is
+ * read once per 32 queries instead of once per query (MFMA tiles).
+ * q, out: fp32 [m][H][D] with row strides q_stride / out_stride floats
+ * (<= 0: H*D), 16-byte aligned.  fp16 pools, head_dim 64 or 128, page_size
+ * 16 or 32 (else LLM_ERR_UNSUPPORTED; pa_decode covers every shape). */
+int pa_prefill(const pa_kv_view* kv, const float* q, int q_stride, float* out, int out_stride,
+               int row, int p0, int m, float sm_scale, void* stream);
+
 /* The optional stages of the reference attention, CPUAttentionInput /
  * CPUAttentionOutput (attention_cpu/attention_cpu.hpp:8-43) as used by
  * cpu_paged_attention_forward (attention_cpu/cpu_attention_kernel.cpp:37-129):

@@ -91,6 +91,7 @@ struct llm_decoder {
   size_t attn_ws_bytes = 0;
 
   int batch = 0;
+  bool prefill_mfma = true;  // LLM_PREFILL_MFMA=0: prompt chunks through the decode kernel
   std::vector<int> h_pos;  // host mirror of the next position of each row
 
   hipGraphExec_t graph = nullptr;
@@ -216,6 +217,7 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   d->microbatches = env_int("LLM_MICROBATCHES", 1);
   d->pingpong = env_int("LLM_MB_PINGPONG", 0) != 0;
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
+  d->prefill_mfma = env_int("LLM_PREFILL_MFMA", 1) != 0;
   d->mb_attn_waves = env_int("LLM_MB_ATTN_WAVES", 0);
   if (d->microbatches >= 2 && B >= 2) {
     LLM_HIP_RET(hipStreamCreateWithFlags(&d->stream2, hipStreamNonBlocking));
@@ -350,6 +352,10 @@ struct Rows {
   int table_row0 = 0;
   int row_group = 1;
   int attn_waves_per_simd = 0;  // > 0: lean attention leaving CU room (micro-batch overlap)
+  // prefill chunk (row >= 0): the n rows are positions p0 .. p0+n-1 of page-table
+  // row prefill_row, attended causally by the MFMA prefill kernel
+  int prefill_row = -1;
+  int prefill_p0 = 0;
   uint8_t* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
 };
@@ -400,6 +406,17 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   RET_IF(kv_cache_view(kv, l, &view));
   view.page_table += (size_t)R.table_row0 * H * view.max_tiles;  // rows of this micro-batch
   view.num_beams -= R.table_row0;
+  if (R.prefill_row >= 0 && prefill_mfma && pa_prefill_supported(&view)) {
+    // one MFMA pass over the chunk (K/V pages read once per 32 queries), then
+    // the o_proj input conversion the decode merge would have fused
+    RET_IF(pa_prefill_internal(&view, R.q, hid, R.o, hid, R.prefill_row, R.prefill_p0, R.n,
+                               cfg.attn_scale, st));
+    if (wdtype == LLM_I8)
+      LLM_HIP_RET(launch_quantize_rows(R.o, R.n, hid, static_cast<int8_t*>(R.act), R.sa, st, 1));
+    else
+      LLM_HIP_RET(launch_to_f16(R.o, (size_t)R.n * hid, R.act, st, hid));
+    return LLM_OK;
+  }
   // the split merge also produces the o_proj input (packed int8 + scale, or fp16)
   PaRowOutputs ro;
   ro.pack = 1;
@@ -654,6 +671,8 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     if (wdtype == LLM_F16)
       R.act2 = pact.p + (((size_t)C + 15) / 16 * 16) * std::max(hid, inter) * 2;
     R.pos = pmeta.p; R.ctx = pmeta.p + C; R.beam_rows = pmeta.p + 2 * C;
+    R.prefill_row = row;
+    R.prefill_p0 = p0;
     R.attn_ws = pws.p; R.attn_ws_bytes = pws_bytes;
     LLM_HIP_RET(launch_embed(emb.p, pmeta.p + 3 * C, m, hid, V, px.p, st));
     for (int l = 0; l < L; ++l) {

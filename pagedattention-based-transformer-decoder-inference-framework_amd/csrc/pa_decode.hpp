@@ -27,6 +27,13 @@ int pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float
                        int waves_per_simd = 0);
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 
+// Causal MFMA attention of a prompt chunk (csrc/pa_prefill.hip, C entry
+// pa_prefill): out rows i < m = attention of query i (position p0 + i) over
+// positions 0 .. p0 + i of page-table row `row`.
+bool pa_prefill_supported(const pa_kv_view* kv);
+int pa_prefill_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
+                        int out_stride, int row, int p0, int m, float sm_scale, hipStream_t st);
+
 // Bytes per element of a KV pool type (0: unknown type).
 inline int kv_elem_size(int kvt) {
   return kvt == LLM_F16 || kvt == LLM_BF16 ? 2 : kvt == LLM_F32 ? 4 : kvt == LLM_I8 ? 1 : 0;

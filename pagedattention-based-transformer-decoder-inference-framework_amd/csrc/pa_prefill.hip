@@ -1,0 +1,325 @@
+// Causal paged attention of a prompt chunk on MFMA (the reference's is_prefill
+// pass: AttentionCUDA's `is_prefill` flag, attention/attention_cuda.hpp:21,
+// with the maths of cpu_paged_attention_forward,
+// attention_cpu/cpu_attention_kernel.cpp:37-129, per query token; SURVEY §8f
+// row 4).
+//
+// m query tokens of ONE sequence sit at positions p0 .. p0+m-1 and their K/V
+// are already in the sequence's pages (page-table row `row`).  Query i attends
+// to positions 0 .. p0+i.  The decode kernel computes the same thing with one
+// wave per (token, head), so each page is re-read once per query token; here a
+// workgroup of NW waves owns 16·NW consecutive queries of one head, stages
+// every 32-key block of K and V into LDS ONCE, and each wave runs
+//   S^T[32 keys][16 queries] = K · Q^T        (v_mfma_f32_16x16x32_f16)
+//   O^T[D][16 queries]     += V^T · P^T
+// with the flash online softmax (log2 units, as pa_split_kernel) in between.
+//
+// Orientation: keys are the MFMA row index of S^T, so the C layout of S^T
+// (lane l: rows 4(l>>4)+r, column l&15) already holds, per lane, 8 keys of ONE
+// query: that is the B operand of the P·V product once the 32 keys are taken
+// in the k order slot(key) = 8·((key&15)>>2) + 4·(key>>4) + (key&3).  V is
+// staged transposed (Vt[d][slot]) in that same order, so the V^T A operand is
+// one 16-byte LDS read per lane.  The query is the lane's column in both
+// products, so the running max / sum / rescale are per lane (the 4 lanes of a
+// query agree after a 2-step max exchange).
+//
+// Accuracy: q (fp32, pre-scaled by sm_scale·log2e) and p (fp32) are split into
+// fp16 hi + lo halves and each product is two MFMAs; K and V are fp16 already.
+// Both are first scaled by a power of two (q per query to |q|max ≈ 2^14, p by
+// 2^14) because the MFMA drops fp16 subnormal inputs: unscaled, the lo half
+// of every p < 0.25 was lost (1e-5 .. 5e-5 output error, measured).  Scaled,
+// products of fp16 pairs are exact in the fp32 accumulator and the output
+// error is at the decode kernel's level (scripts/diag_prefill.py).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "common.hpp"
+#include "pa_decode.hpp"
+
+namespace llm {
+namespace {
+
+struct PaPrefillArgs {
+  const float* q;
+  int q_stride;  // floats between query rows
+  float* out;
+  int out_stride;
+  const uint8_t* k_pool;
+  const uint8_t* v_pool;
+  size_t page_stride;     // bytes
+  const int32_t* pt_row;  // page_table + row * H * max_tiles
+  int H, max_tiles, num_pages;
+  int p0, m;
+  float qscale;  // sm_scale * log2(e)
+};
+
+constexpr int kKeyBlock = 32;
+constexpr float kPScale = 16384.f;  // P enters the PV MFMA as p * 2^14 (hi + lo)
+
+__device__ __forceinline__ void split_f16(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
+template <int D, int TS, int NW>
+__global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
+  constexpr int KB = kKeyBlock;
+  constexpr int KSTR = D + 8;   // K row stride (halves): conflict-free 16-B row reads
+  constexpr int VSTR = KB + 8;  // V^T row stride (halves): conflict-free 16-B reads
+  constexpr int CPR = D / 8;    // 16-byte chunks per key row
+  constexpr int NCH = KB * CPR; // chunks per block, each of K and V
+  constexpr int NTH = 64 * NW;
+  constexpr int CPT = NCH / NTH;
+  constexpr int NKK = D / 32;   // k-steps of q.k
+  constexpr int ND = D / 16;    // 16-dim tiles of the output
+  static_assert(NCH % NTH == 0 && D % 32 == 0 && KB % TS == 0, "shape");
+  __shared__ __attribute__((aligned(16))) _Float16 Ks[KB * KSTR];
+  __shared__ __attribute__((aligned(16))) _Float16 Vt[D * VSTR];
+  __shared__ int kval[KB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = wave_id_uniform();
+  const int g = lane >> 4;
+  const int c = lane & 15;
+  const int h = blockIdx.y;
+  const int qbase = blockIdx.x * 16 * NW;
+  const int qi = qbase + w * 16 + c;  // this lane's query (column of S^T / O^T)
+  const int qpos = a.p0 + qi;
+  const int lastpos = a.p0 + min(qbase + 16 * NW, a.m) - 1;  // last key any query here sees
+  const int nblk = lastpos / KB + 1;
+  const int32_t* pt = a.pt_row + (size_t)h * a.max_tiles;
+
+  // Q^T B-operand fragments: lane holds q[qi][32kk + 8g .. +7] (pre-scaled by
+  // qscale), hi + lo.  The query's values are also scaled by a power of two
+  // 2^(14-e) (|q|max < 2^e) so the lo halves stay clear of fp16 subnormals,
+  // which the MFMA does not keep; S is scaled back exactly after the MFMA.
+  float qx[NKK][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk) {
+    f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+    if (qi < a.m) {
+      const float* qp = a.q + (size_t)qi * a.q_stride + h * D + 32 * kk + 8 * g;
+      x0 = *reinterpret_cast<const f32x4*>(qp);
+      x1 = *reinterpret_cast<const f32x4*>(qp + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qx[kk][e] = x0[e] * a.qscale;
+      qx[kk][4 + e] = x1[e] * a.qscale;
+      amax = fmaxf(amax, fmaxf(fabsf(qx[kk][e]), fabsf(qx[kk][4 + e])));
+    }
+  }
+  amax = fmaxf(amax, __shfl_xor(amax, 16, 64));
+  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  int qe = 0;
+  (void)frexpf(amax, &qe);  // amax < 2^qe (0 for amax == 0)
+  qe = min(max(qe, -100), 100);
+  const float qsc = ldexpf(1.f, 14 - qe), qinv = ldexpf(1.f, qe - 14);
+  f16x8 qh[NKK], ql[NKK];
+#pragma unroll
+  for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      _Float16 hi, lo;
+      split_f16(qx[kk][e] * qsc, hi, lo);
+      qh[kk][e] = hi;
+      ql[kk][e] = lo;
+    }
+
+  // Staging: K chunk i of a thread = (key ch / CPR, dims 8 (ch % CPR)) — rows
+  // coalesced; V chunk i = (key ch % KB, dims 8 (ch / KB)) — the 32 keys of a
+  // dim group on adjacent lanes, so the transposed 2-byte LDS writes of a wave
+  // hit distinct slots of one V^T row.
+  u32x4 kr[CPT], vr[CPT];
+  int vok[CPT];
+  auto page_of = [&](int kg) -> int {  // page of key position kg, -1 if none / past lastpos
+    const int tile = kg / TS;
+    int pg = (kg <= lastpos && tile < a.max_tiles) ? pt[tile] : -1;
+    return (pg >= 0 && pg < a.num_pages) ? pg : -1;
+  };
+  auto load = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int ch = tid + i * NTH;
+      {
+        const int key = ch / CPR, d0 = (ch % CPR) * 8;
+        const int kg = kb * KB + key;
+        const int pg = page_of(kg);
+        kr[i] = pg >= 0 ? *reinterpret_cast<const u32x4*>(
+                              a.k_pool + (size_t)pg * a.page_stride + ((kg % TS) * D + d0) * 2)
+                        : u32x4{0u, 0u, 0u, 0u};
+      }
+      {
+        const int key = ch % KB, d0 = (ch / KB) * 8;
+        const int kg = kb * KB + key;
+        const int pg = page_of(kg);
+        vok[i] = pg >= 0;
+        // masked keys stage V = 0: a never-written row may hold NaN (0 * NaN)
+        vr[i] = pg >= 0 ? *reinterpret_cast<const u32x4*>(
+                              a.v_pool + (size_t)pg * a.page_stride + ((kg % TS) * D + d0) * 2)
+                        : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int ch = tid + i * NTH;
+      {
+        const int key = ch / CPR, d0 = (ch % CPR) * 8;
+        *reinterpret_cast<u32x4*>(&Ks[key * KSTR + d0]) = kr[i];
+      }
+      {
+        const int key = ch % KB, d0 = (ch / KB) * 8;
+        const int slot = 8 * ((key & 15) >> 2) + 4 * (key >> 4) + (key & 3);
+        const f16x8 v = __builtin_bit_cast(f16x8, vr[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Vt[(d0 + e) * VSTR + slot] = v[e];
+        if (d0 == 0) kval[key] = vok[i];
+      }
+    }
+  };
+
+  f32x4 O[ND];
+#pragma unroll
+  for (int nd = 0; nd < ND; ++nd) O[nd] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrun = kNegSentinel, lrun = 0.f;
+
+  load(0);
+  for (int kb = 0; kb < nblk; ++kb) {
+    if (kb > 0) __syncthreads();  // every wave is done reading block kb-1
+    stage();
+    __syncthreads();
+    if (kb + 1 < nblk) load(kb + 1);  // next block's loads fly during this block's math
+
+    // S^T: two 16-key tiles
+    f32x4 s[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(&Ks[(16 * t + c) * KSTR + 32 * kk + 8 * g]);
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qh[kk], s[t], 0, 0, 0);
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, ql[kk], s[t], 0, 0, 0);
+      }
+      s[t] *= qinv;
+    }
+    // causal + missing-page mask, online softmax (per query = per lane)
+    bool ok[2][4];
+    float mloc = kNegSentinel;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * t + 4 * g + r;
+        ok[t][r] = kval[key] != 0 && kb * KB + key <= qpos;
+        if (ok[t][r]) mloc = fmaxf(mloc, s[t][r]);
+      }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float mnew = fmaxf(mrun, mloc);
+    const float corr = __builtin_amdgcn_exp2f(mrun - mnew);
+    lrun *= corr;
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) O[nd] *= corr;
+    f16x8 ph, pl;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = ok[t][r] ? __builtin_amdgcn_exp2f(s[t][r] - mnew) : 0.f;
+        lrun += p;
+        _Float16 hi, lo;
+        split_f16(p * kPScale, hi, lo);  // p <= 1: scaled clear of fp16 subnormals
+        ph[4 * t + r] = hi;
+        pl[4 * t + r] = lo;
+      }
+    mrun = mnew;
+    // O^T += V^T · P^T
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) {
+      const f16x8 vf = *reinterpret_cast<const f16x8*>(&Vt[(16 * nd + c) * VSTR + 8 * g]);
+      O[nd] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, ph, O[nd], 0, 0, 0);
+      O[nd] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pl, O[nd], 0, 0, 0);
+    }
+  }
+
+  // the 4 lanes of a query hold partial sums over their keys
+  lrun += __shfl_xor(lrun, 16, 64);
+  lrun += __shfl_xor(lrun, 32, 64);
+  if (qi < a.m) {
+    const float inv = 1.0f / (lrun + 1e-6f) * (1.0f / kPScale);
+    float* o = a.out + (size_t)qi * a.out_stride + h * D + 4 * g;
+#pragma unroll
+    for (int nd = 0; nd < ND; ++nd) *reinterpret_cast<f32x4*>(o + 16 * nd) = O[nd] * inv;
+  }
+}
+
+template <int D, int TS>
+hipError_t launch_prefill(const PaPrefillArgs& a, hipStream_t st) {
+  constexpr int NW = 2;
+  const dim3 grid((a.m + 16 * NW - 1) / (16 * NW), a.H);
+  hipLaunchKernelGGL((pa_prefill_kernel<D, TS, NW>), grid, dim3(64 * NW), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool pa_prefill_supported(const pa_kv_view* kv) {
+  return kv && kv->kv_dtype == LLM_F16 && (kv->head_dim == 64 || kv->head_dim == 128) &&
+         (kv->page_size == 16 || kv->page_size == 32);
+}
+
+int pa_prefill_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
+                        int out_stride, int row, int p0, int m, float sm_scale, hipStream_t st) {
+  LLM_REQUIRE(kv && q && out, "pa_prefill: NULL argument");
+  if (!pa_prefill_supported(kv))
+    return fail(LLM_ERR_UNSUPPORTED,
+                "pa_prefill: fp16 pools with head_dim 64 or 128 and page_size 16 or 32 only");
+  const int H = kv->num_heads, D = kv->head_dim;
+  LLM_REQUIRE(m >= 1 && p0 >= 0, "pa_prefill: need m >= 1 and p0 >= 0");
+  LLM_REQUIRE(row >= 0 && row < kv->num_beams, "pa_prefill: row outside the page table");
+  LLM_REQUIRE((long long)(p0 + m + kv->page_size - 1) / kv->page_size <= kv->max_tiles,
+              "pa_prefill: positions past the page table's max_tiles");
+  if (q_stride <= 0) q_stride = H * D;
+  if (out_stride <= 0) out_stride = H * D;
+  LLM_REQUIRE(q_stride >= H * D && out_stride >= H * D && q_stride % 4 == 0 && out_stride % 4 == 0,
+              "pa_prefill: row strides must be >= H*D and multiples of 4");
+  LLM_REQUIRE(reinterpret_cast<uintptr_t>(q) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0,
+              "pa_prefill: q and out must be 16-byte aligned");
+  PaPrefillArgs a{};
+  a.q = q;
+  a.q_stride = q_stride;
+  a.out = out;
+  a.out_stride = out_stride;
+  a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
+  a.v_pool = static_cast<const uint8_t*>(kv->v_pool);
+  a.page_stride = kv_view_page_stride(*kv);
+  a.pt_row = kv->page_table + (size_t)row * H * kv->max_tiles;
+  a.H = H;
+  a.max_tiles = kv->max_tiles;
+  a.num_pages = kv->num_pages;
+  a.p0 = p0;
+  a.m = m;
+  a.qscale = sm_scale * kLog2e;
+  hipError_t e;
+  const int TS = kv->page_size;
+  if (D == 64)
+    e = TS == 16 ? launch_prefill<64, 16>(a, st) : launch_prefill<64, 32>(a, st);
+  else
+    e = TS == 16 ? launch_prefill<128, 16>(a, st) : launch_prefill<128, 32>(a, st);
+  if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_prefill launch: ") + hipGetErrorString(e));
+  return LLM_OK;
+}
+
+}  // namespace llm
+
+extern "C" int pa_prefill(const pa_kv_view* kv, const float* q, int q_stride, float* out,
+                          int out_stride, int row, int p0, int m, float sm_scale, void* stream) {
+  return llm::pa_prefill_internal(kv, q, q_stride, out, out_stride, row, p0, m, sm_scale,
+                                  llm::as_stream(stream));
+}

@@ -62,6 +62,8 @@ _SIGS = {
     "pa_decode_ex": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p, c_void_p,
                              c_int, c_int, c_int, c_int, ctypes.POINTER(PaDecodeOptions),
                              c_void_p, c_size_t, c_void_p]),
+    "pa_prefill": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_int, c_void_p, c_int, c_int,
+                           c_int, c_int, c_float, c_void_p]),
     "gemm_packed_bytes": (c_size_t, [c_int, c_int, c_int]),
     "gemm_pack_weights": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "i8_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -231,6 +233,26 @@ def pa_decode_ex(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_len
     check(lib.pa_decode_ex(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids), ptr(context_lens),
                            B, H, D, T, ctypes.byref(opt), ptr(ws), ws_bytes, stream_ptr(stream)))
     return (out, probs, scores) if want_probs else out
+
+
+def pa_prefill(q, k_pool, v_pool, page_table, *, row, p0, sm_scale=1.0, out=None,
+               stream=None):
+    """Causal attention of a prompt chunk (pa_prefill): q [m][H][D] (or a
+    [m][stride] row view whose first H*D floats are the heads) at positions
+    p0 .. p0+m-1 of page-table row `row`; returns out [m][H][D] fp32."""
+    import torch
+    lib = load()
+    m = q.shape[0]
+    H, D = page_table.shape[1], k_pool.shape[2]
+    q_stride = q.stride(0)
+    if q.stride(-1) != 1:
+        raise ValueError("q rows must be contiguous")
+    if out is None:
+        out = torch.empty((m, H, D), dtype=torch.float32, device=q.device)
+    view = kv_view(k_pool, v_pool, page_table)
+    check(lib.pa_prefill(ctypes.byref(view), ptr(q), q_stride, ptr(out), out.stride(0), row, p0,
+                         m, sm_scale, stream_ptr(stream)))
+    return out
 
 
 def pack_weights(W, dtype: int, stream=None):
