@@ -116,9 +116,14 @@ int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* out, const in
  * read once per 32 queries instead of once per query (MFMA tiles).
  * q, out: fp32 [m][H][D] with row strides q_stride / out_stride floats
  * (<= 0: H*D), 16-byte aligned.  fp16 pools, head_dim 64 or 128, page_size
- * 16 or 32 (else LLM_ERR_UNSUPPORTED; pa_decode covers every shape). */
+ * 16 or 32 (else LLM_ERR_UNSUPPORTED; pa_decode covers every shape).
+ * With workspace_bytes >= pa_prefill_workspace_bytes(kv, p0, m) (and
+ * out_stride H*D) the key range is split over more workgroups and merged as
+ * pa_decode's splits; with less (or NULL) it runs in one pass. */
+size_t pa_prefill_workspace_bytes(const pa_kv_view* kv, int p0, int m);
 int pa_prefill(const pa_kv_view* kv, const float* q, int q_stride, float* out, int out_stride,
-               int row, int p0, int m, float sm_scale, void* stream);
+               int row, int p0, int m, float sm_scale, void* workspace, size_t workspace_bytes,
+               void* stream);
 
 /* The optional stages of the reference attention, CPUAttentionInput /
  * CPUAttentionOutput (attention_cpu/attention_cpu.hpp:8-43) as used by

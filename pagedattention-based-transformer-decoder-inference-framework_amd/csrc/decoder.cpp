@@ -409,13 +409,16 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   if (R.prefill_row >= 0 && prefill_mfma && pa_prefill_supported(&view)) {
     // one MFMA pass over the chunk (K/V pages read once per 32 queries), then
     // the o_proj input conversion the decode merge would have fused
-    RET_IF(pa_prefill_internal(&view, R.q, hid, R.o, hid, R.prefill_row, R.prefill_p0, R.n,
-                               cfg.attn_scale, st));
-    if (wdtype == LLM_I8)
-      LLM_HIP_RET(launch_quantize_rows(R.o, R.n, hid, static_cast<int8_t*>(R.act), R.sa, st, 1));
-    else
-      LLM_HIP_RET(launch_to_f16(R.o, (size_t)R.n * hid, R.act, st, hid));
-    return LLM_OK;
+    PaRowOutputs ro;
+    ro.pack = 1;
+    if (wdtype == LLM_I8) {
+      ro.q = static_cast<int8_t*>(R.act);
+      ro.inv_scale = R.sa;
+    } else {
+      ro.out16 = R.act;
+    }
+    return pa_prefill_internal(&view, R.q, hid, R.o, hid, R.prefill_row, R.prefill_p0, R.n,
+                               cfg.attn_scale, R.attn_ws, R.attn_ws_bytes, st, &ro);
   }
   // the split merge also produces the o_proj input (packed int8 + scale, or fp16)
   PaRowOutputs ro;
@@ -644,6 +647,12 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     pws_bytes = 16;
     for (int b = 1; b <= C; ++b)
       pws_bytes = std::max(pws_bytes, pa_decode_workspace_bytes(b, H, D, max_tiles, 0));
+    {  // the MFMA prefill's split partials (its split count is bounded at any p0)
+      pa_kv_view v0;
+      RET_IF(kv_cache_view(kv, 0, &v0));
+      for (int b = 1; b <= C; ++b)
+        pws_bytes = std::max(pws_bytes, pa_prefill_ws_bytes(&v0, cfg.max_seq_len - b, b));
+    }
     RET_IF(pws.alloc(pws_bytes));
     pf_cap = C;
   }

@@ -496,6 +496,7 @@ struct PaMergeRowArgs {
   const int32_t* context_lens;
   int B, H, D, T, TS, pps, nsplit, max_tiles;
   int pack;  // q / out16 in packed-A order (common.hpp a_frag_off_*)
+  int ctx_p0;  // >= 0 and context_lens NULL: row b's context is ctx_p0 + b + 1 (prefill)
 };
 
 // DPL = output dims per lane (D / 64, at least 1).  A head's split weights
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   const int nw = blockDim.x >> 6;
   const int b = blockIdx.x;
   const int hid = a.H * a.D;
-  int Tb = a.context_lens ? a.context_lens[b] : a.T;
+  int Tb = a.context_lens ? a.context_lens[b] : a.ctx_p0 >= 0 ? a.ctx_p0 + b + 1 : a.T;
   Tb = min(max(Tb, 0), a.T);
   const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
   const int pps = row_pps(a.pps, a.nsplit, ntiles);
@@ -811,6 +812,26 @@ extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
   return (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
 }
 
+int llm::pa_merge_rows_internal(const float* part_acc, const float* part_ml, float* out,
+                                const PaRowOutputs* rows, const int32_t* context_lens, int ctx_p0,
+                                int B, int H, int D, int T, int TS, int pps, int nsplit,
+                                int max_tiles, hipStream_t st) {
+  PaMergeRowArgs mg{part_acc, part_ml, out, rows ? rows->q : nullptr,
+                    rows ? rows->inv_scale : nullptr,
+                    rows ? static_cast<_Float16*>(rows->out16) : nullptr, context_lens, B, H, D, T,
+                    TS, pps, nsplit, max_tiles, rows ? rows->pack : 0, ctx_p0};
+  const int threads = 64 * std::min(16, H);  // one wave per head (heads > 16 loop)
+  const size_t lds = (size_t)H * D * sizeof(float);
+  if (D <= 64)
+    hipLaunchKernelGGL(pa_merge_row_kernel<1>, dim3(B), dim3(threads), lds, st, mg);
+  else if (D <= 128)
+    hipLaunchKernelGGL(pa_merge_row_kernel<2>, dim3(B), dim3(threads), lds, st, mg);
+  else
+    hipLaunchKernelGGL(pa_merge_row_kernel<4>, dim3(B), dim3(threads), lds, st, mg);
+  LLM_HIP_RET(hipGetLastError());
+  return LLM_OK;
+}
+
 int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                             int D, int T, float sm_scale, int pages_per_split, void* workspace,
@@ -900,21 +921,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, lean, st); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
-  if (row_out && !direct) {
-    PaMergeRowArgs mg{a.part_acc, a.part_ml, out, rows->q, rows->inv_scale,
-                      static_cast<_Float16*>(rows->out16), context_lens, B, H, D, T, TS, pps_fixed,
-                      nsplit, kv->max_tiles, rows->pack};
-    const int threads = 64 * std::min(16, H);  // one wave per head (heads > 16 loop)
-    const size_t lds = (size_t)H * D * sizeof(float);
-    if (D <= 64)
-      hipLaunchKernelGGL(pa_merge_row_kernel<1>, dim3(B), dim3(threads), lds, st, mg);
-    else if (D <= 128)
-      hipLaunchKernelGGL(pa_merge_row_kernel<2>, dim3(B), dim3(threads), lds, st, mg);
-    else
-      hipLaunchKernelGGL(pa_merge_row_kernel<4>, dim3(B), dim3(threads), lds, st, mg);
-    LLM_HIP_RET(hipGetLastError());
-    return LLM_OK;
-  }
+  if (row_out && !direct)
+    return pa_merge_rows_internal(a.part_acc, a.part_ml, out, rows, context_lens, -1, B, H, D, T,
+                                  TS, pps_fixed, nsplit, kv->max_tiles, st);
   if (!direct) {
     PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, TS, pps_fixed, nsplit,
                    kv->max_tiles};

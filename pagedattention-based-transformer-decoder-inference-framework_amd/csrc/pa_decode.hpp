@@ -27,12 +27,27 @@ int pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float
                        int waves_per_simd = 0);
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 
+// Split merge of per-(row, head, split) partial softmax states into rows
+// (out fp32 [B][H*D] and/or the rows->q / out16 o_proj inputs); row b's
+// context is context_lens[b], or ctx_p0 + b + 1 when context_lens is NULL and
+// ctx_p0 >= 0, or T.  Split s of a row covers tiles [s*pps, (s+1)*pps).
+int pa_merge_rows_internal(const float* part_acc, const float* part_ml, float* out,
+                           const PaRowOutputs* rows, const int32_t* context_lens, int ctx_p0,
+                           int B, int H, int D, int T, int TS, int pps, int nsplit, int max_tiles,
+                           hipStream_t st);
+
 // Causal MFMA attention of a prompt chunk (csrc/pa_prefill.hip, C entry
 // pa_prefill): out rows i < m = attention of query i (position p0 + i) over
 // positions 0 .. p0 + i of page-table row `row`.
+// With workspace (pa_prefill_workspace_bytes) the key range is split over
+// workgroups and merged by pa_merge_rows_internal, which also writes `rows`
+// (the o_proj input); without, one pass writes out and `rows` is converted by
+// the row quantiser.  `out` may be NULL only when it splits and rows is set.
 bool pa_prefill_supported(const pa_kv_view* kv);
+size_t pa_prefill_ws_bytes(const pa_kv_view* kv, int p0, int m);
 int pa_prefill_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
-                        int out_stride, int row, int p0, int m, float sm_scale, hipStream_t st);
+                        int out_stride, int row, int p0, int m, float sm_scale, void* workspace,
+                        size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows = nullptr);
 
 // Bytes per element of a KV pool type (0: unknown type).
 inline int kv_elem_size(int kvt) {

@@ -36,6 +36,7 @@
 
 #include "common.hpp"
 #include "pa_decode.hpp"
+#include "row_ops.hpp"
 
 namespace llm {
 namespace {
@@ -52,6 +53,12 @@ struct PaPrefillArgs {
   int H, max_tiles, num_pages;
   int p0, m;
   float qscale;  // sm_scale * log2(e)
+  // key-range split (blockIdx.z = split s: tiles [s*pps, (s+1)*pps)); with
+  // part_acc the unnormalised state goes to the decode layout
+  // [(i*H + h)*nsplit + s][D] / [..][2] (m, l) for pa_merge_rows_internal
+  int nsplit, pps;
+  float* part_acc;
+  float* part_ml;
 };
 
 constexpr int kKeyBlock = 32;
@@ -88,7 +95,11 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
   const int qi = qbase + w * 16 + c;  // this lane's query (column of S^T / O^T)
   const int qpos = a.p0 + qi;
   const int lastpos = a.p0 + min(qbase + 16 * NW, a.m) - 1;  // last key any query here sees
-  const int nblk = lastpos / KB + 1;
+  const int split = blockIdx.z;
+  const int kb0 = split * a.pps * TS / KB;
+  const int nblk = min((split + 1) * a.pps * TS / KB, lastpos / KB + 1);
+  // no query of this workgroup reaches this split: the merge never reads it
+  if (kb0 >= nblk) return;
   const int32_t* pt = a.pt_row + (size_t)h * a.max_tiles;
 
   // Q^T B-operand fragments: lane holds q[qi][32kk + 8g .. +7] (pre-scaled by
@@ -188,9 +199,9 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
   for (int nd = 0; nd < ND; ++nd) O[nd] = f32x4{0.f, 0.f, 0.f, 0.f};
   float mrun = kNegSentinel, lrun = 0.f;
 
-  load(0);
-  for (int kb = 0; kb < nblk; ++kb) {
-    if (kb > 0) __syncthreads();  // every wave is done reading block kb-1
+  load(kb0);
+  for (int kb = kb0; kb < nblk; ++kb) {
+    if (kb > kb0) __syncthreads();  // every wave is done reading block kb-1
     stage();
     __syncthreads();
     if (kb + 1 < nblk) load(kb + 1);  // next block's loads fly during this block's math
@@ -252,19 +263,57 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
   lrun += __shfl_xor(lrun, 16, 64);
   lrun += __shfl_xor(lrun, 32, 64);
   if (qi < a.m) {
-    const float inv = 1.0f / (lrun + 1e-6f) * (1.0f / kPScale);
-    float* o = a.out + (size_t)qi * a.out_stride + h * D + 4 * g;
+    if (a.part_acc) {  // split partial state (unnormalised, log2 units)
+      const size_t pidx = ((size_t)qi * a.H + h) * a.nsplit + split;
+      float* o = a.part_acc + pidx * D + 4 * g;
 #pragma unroll
-    for (int nd = 0; nd < ND; ++nd) *reinterpret_cast<f32x4*>(o + 16 * nd) = O[nd] * inv;
+      for (int nd = 0; nd < ND; ++nd) *reinterpret_cast<f32x4*>(o + 16 * nd) = O[nd] * (1.0f / kPScale);
+      if (g == 0) *reinterpret_cast<float2*>(a.part_ml + pidx * 2) = float2{mrun, lrun};
+    } else {
+      const float inv = 1.0f / (lrun + 1e-6f) * (1.0f / kPScale);
+      float* o = a.out + (size_t)qi * a.out_stride + h * D + 4 * g;
+#pragma unroll
+      for (int nd = 0; nd < ND; ++nd) *reinterpret_cast<f32x4*>(o + 16 * nd) = O[nd] * inv;
+    }
   }
 }
 
 template <int D, int TS>
-hipError_t launch_prefill(const PaPrefillArgs& a, hipStream_t st) {
-  constexpr int NW = 2;
-  const dim3 grid((a.m + 16 * NW - 1) / (16 * NW), a.H);
-  hipLaunchKernelGGL((pa_prefill_kernel<D, TS, NW>), grid, dim3(64 * NW), 0, st, a);
+hipError_t launch_prefill(const PaPrefillArgs& a, int nw, hipStream_t st) {
+  if (nw == 4) {
+    const dim3 grid((a.m + 63) / 64, a.H, a.nsplit);
+    hipLaunchKernelGGL((pa_prefill_kernel<D, TS, 4>), grid, dim3(256), 0, st, a);
+  } else {
+    const dim3 grid((a.m + 31) / 32, a.H, a.nsplit);
+    hipLaunchKernelGGL((pa_prefill_kernel<D, TS, 2>), grid, dim3(128), 0, st, a);
+  }
   return hipGetLastError();
+}
+
+// Launch geometry: NW waves (16 queries each) per workgroup; the key range is
+// split until the grid holds about kTargetWgs workgroups (4 per CU), in
+// splits of whole 32-key blocks and at least 2 blocks each.
+constexpr int kTargetWgs = 1024;
+struct PrefillPlan {
+  int nw, nsplit, pps;
+};
+PrefillPlan prefill_plan(const pa_kv_view* kv, int p0, int m) {
+  PrefillPlan p;
+  p.nw = env_int("LLM_PREFILL_NW", 4) == 2 ? 2 : 4;
+  const int TS = kv->page_size;
+  const int step = kKeyBlock / TS;  // tiles per key block
+  const int ntiles = (p0 + m + TS - 1) / TS;
+  const int nq = (m + 16 * p.nw - 1) / (16 * p.nw);
+  const int want = std::min(std::max(kTargetWgs / std::max(nq * kv->num_heads, 1), 1), 128);
+  int pps = (ntiles + want - 1) / want;
+  pps = std::max((pps + step - 1) / step * step, 2 * step);
+  p.pps = pps;
+  p.nsplit = std::max(1, std::min((ntiles + pps - 1) / pps, 128));
+  if (p.nsplit * pps < ntiles) {  // > 128 splits: lengthen them
+    p.pps = ((ntiles + 127) / 128 + step - 1) / step * step;
+    p.nsplit = (ntiles + p.pps - 1) / p.pps;
+  }
+  return p;
 }
 
 }  // namespace
@@ -274,23 +323,38 @@ bool pa_prefill_supported(const pa_kv_view* kv) {
          (kv->page_size == 16 || kv->page_size == 32);
 }
 
+size_t pa_prefill_ws_bytes(const pa_kv_view* kv, int p0, int m) {
+  if (!pa_prefill_supported(kv) || m <= 0 || p0 < 0) return 0;
+  const PrefillPlan p = prefill_plan(kv, p0, m);
+  if (p.nsplit <= 1) return 0;
+  return (size_t)m * kv->num_heads * p.nsplit * (size_t)(kv->head_dim + 2) * sizeof(float);
+}
+
 int pa_prefill_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
-                        int out_stride, int row, int p0, int m, float sm_scale, hipStream_t st) {
-  LLM_REQUIRE(kv && q && out, "pa_prefill: NULL argument");
+                        int out_stride, int row, int p0, int m, float sm_scale, void* workspace,
+                        size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows) {
+  LLM_REQUIRE(kv && q, "pa_prefill: NULL argument");
   if (!pa_prefill_supported(kv))
     return fail(LLM_ERR_UNSUPPORTED,
                 "pa_prefill: fp16 pools with head_dim 64 or 128 and page_size 16 or 32 only");
-  const int H = kv->num_heads, D = kv->head_dim;
+  const int H = kv->num_heads, D = kv->head_dim, hid = H * D;
   LLM_REQUIRE(m >= 1 && p0 >= 0, "pa_prefill: need m >= 1 and p0 >= 0");
   LLM_REQUIRE(row >= 0 && row < kv->num_beams, "pa_prefill: row outside the page table");
   LLM_REQUIRE((long long)(p0 + m + kv->page_size - 1) / kv->page_size <= kv->max_tiles,
               "pa_prefill: positions past the page table's max_tiles");
-  if (q_stride <= 0) q_stride = H * D;
-  if (out_stride <= 0) out_stride = H * D;
-  LLM_REQUIRE(q_stride >= H * D && out_stride >= H * D && q_stride % 4 == 0 && out_stride % 4 == 0,
+  if (q_stride <= 0) q_stride = hid;
+  if (out_stride <= 0) out_stride = hid;
+  LLM_REQUIRE(q_stride >= hid && out_stride >= hid && q_stride % 4 == 0 && out_stride % 4 == 0,
               "pa_prefill: row strides must be >= H*D and multiples of 4");
   LLM_REQUIRE(reinterpret_cast<uintptr_t>(q) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0,
               "pa_prefill: q and out must be 16-byte aligned");
+  const bool row_out = rows && (rows->q || rows->out16);
+  PrefillPlan pl = prefill_plan(kv, p0, m);
+  const size_t need = pa_prefill_ws_bytes(kv, p0, m);
+  const bool split = pl.nsplit > 1 && workspace && workspace_bytes >= need &&
+                     (out == nullptr || out_stride == hid) &&
+                     (!row_out || rows->pack);  // the merge writes packed o_proj inputs
+  LLM_REQUIRE(out || (split && row_out), "pa_prefill: out is NULL");
   PaPrefillArgs a{};
   a.q = q;
   a.q_stride = q_stride;
@@ -306,20 +370,44 @@ int pa_prefill_internal(const pa_kv_view* kv, const float* q, int q_stride, floa
   a.p0 = p0;
   a.m = m;
   a.qscale = sm_scale * kLog2e;
+  if (split) {
+    a.nsplit = pl.nsplit;
+    a.pps = pl.pps;
+    a.part_acc = static_cast<float*>(workspace);
+    a.part_ml = a.part_acc + (size_t)m * H * pl.nsplit * D;
+  } else {
+    a.nsplit = 1;
+    a.pps = kv->max_tiles;
+  }
   hipError_t e;
   const int TS = kv->page_size;
   if (D == 64)
-    e = TS == 16 ? launch_prefill<64, 16>(a, st) : launch_prefill<64, 32>(a, st);
+    e = TS == 16 ? launch_prefill<64, 16>(a, pl.nw, st) : launch_prefill<64, 32>(a, pl.nw, st);
   else
-    e = TS == 16 ? launch_prefill<128, 16>(a, st) : launch_prefill<128, 32>(a, st);
+    e = TS == 16 ? launch_prefill<128, 16>(a, pl.nw, st) : launch_prefill<128, 32>(a, pl.nw, st);
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_prefill launch: ") + hipGetErrorString(e));
+  if (split)
+    return pa_merge_rows_internal(a.part_acc, a.part_ml, out, rows, nullptr, p0, m, H, D,
+                                  p0 + m, TS, pl.pps, pl.nsplit, kv->max_tiles, st);
+  if (row_out) {  // one pass: convert the fp32 rows into the o_proj input
+    if (rows->q)
+      LLM_HIP_RET(launch_quantize_rows(out, m, hid, rows->q, rows->inv_scale, st, rows->pack));
+    if (rows->out16)
+      LLM_HIP_RET(launch_to_f16(out, (size_t)m * hid, rows->out16, st, rows->pack ? hid : 0));
+  }
   return LLM_OK;
 }
 
 }  // namespace llm
 
+extern "C" size_t pa_prefill_workspace_bytes(const pa_kv_view* kv, int p0, int m) {
+  return llm::pa_prefill_ws_bytes(kv, p0, m);
+}
+
 extern "C" int pa_prefill(const pa_kv_view* kv, const float* q, int q_stride, float* out,
-                          int out_stride, int row, int p0, int m, float sm_scale, void* stream) {
+                          int out_stride, int row, int p0, int m, float sm_scale, void* workspace,
+                          size_t workspace_bytes, void* stream) {
+  LLM_REQUIRE(out, "pa_prefill: out is NULL");
   return llm::pa_prefill_internal(kv, q, q_stride, out, out_stride, row, p0, m, sm_scale,
-                                  llm::as_stream(stream));
+                                  workspace, workspace_bytes, llm::as_stream(stream));
 }

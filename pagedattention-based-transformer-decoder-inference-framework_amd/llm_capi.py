@@ -62,8 +62,9 @@ _SIGS = {
     "pa_decode_ex": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p, c_void_p,
                              c_int, c_int, c_int, c_int, ctypes.POINTER(PaDecodeOptions),
                              c_void_p, c_size_t, c_void_p]),
+    "pa_prefill_workspace_bytes": (c_size_t, [ctypes.POINTER(PaKvView), c_int, c_int]),
     "pa_prefill": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_int, c_void_p, c_int, c_int,
-                           c_int, c_int, c_float, c_void_p]),
+                           c_int, c_int, c_float, c_void_p, c_size_t, c_void_p]),
     "gemm_packed_bytes": (c_size_t, [c_int, c_int, c_int]),
     "gemm_pack_weights": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "i8_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -236,10 +237,11 @@ def pa_decode_ex(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_len
 
 
 def pa_prefill(q, k_pool, v_pool, page_table, *, row, p0, sm_scale=1.0, out=None,
-               stream=None):
+               split=True, stream=None):
     """Causal attention of a prompt chunk (pa_prefill): q [m][H][D] (or a
     [m][stride] row view whose first H*D floats are the heads) at positions
-    p0 .. p0+m-1 of page-table row `row`; returns out [m][H][D] fp32."""
+    p0 .. p0+m-1 of page-table row `row`; returns out [m][H][D] fp32.
+    split=False runs the one-pass form (no workspace)."""
     import torch
     lib = load()
     m = q.shape[0]
@@ -250,8 +252,10 @@ def pa_prefill(q, k_pool, v_pool, page_table, *, row, p0, sm_scale=1.0, out=None
     if out is None:
         out = torch.empty((m, H, D), dtype=torch.float32, device=q.device)
     view = kv_view(k_pool, v_pool, page_table)
+    ws_bytes = lib.pa_prefill_workspace_bytes(ctypes.byref(view), p0, m) if split else 0
+    ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=q.device) if ws_bytes else None
     check(lib.pa_prefill(ctypes.byref(view), ptr(q), q_stride, ptr(out), out.stride(0), row, p0,
-                         m, sm_scale, stream_ptr(stream)))
+                         m, sm_scale, ptr(ws), ws_bytes, stream_ptr(stream)))
     return out
 
 

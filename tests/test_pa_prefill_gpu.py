@@ -62,13 +62,17 @@ def _oracle(oracle, q, kp, vp, pt, row, p0, sm_scale=1.0):
     (2, 128, 16, 1000, 200, 1), # later chunk: long prefix, ragged tail page
     (2, 128, 32, 517, 96, 0),   # page 32
     (2, 64, 32, 31, 1, 1),
+    (16, 128, 16, 7680, 512, 0),  # C3 heads, the last chunk of an 8192-token prompt
 ])
-def test_pa_prefill_vs_oracle(gpu, oracle, H, D, ts, p0, m, row):
+@pytest.mark.parametrize("split", [True, False])
+def test_pa_prefill_vs_oracle(gpu, oracle, H, D, ts, p0, m, row, split):
+    """split: key range over several workgroups + the decode merge; else one pass."""
     import llm_capi
     rng = np.random.default_rng(p0 * 7 + m + D)
     kp, vp, pt = _case(rng, rows=3, H=H, D=D, T=p0 + m, ts=ts, nan_tail=True)
     q = (rng.standard_normal((m, H, D)) * D ** -0.25).astype(np.float32)
-    out = llm_capi.pa_prefill(_dev(q), _dev(kp), _dev(vp), _dev(pt), row=row, p0=p0).cpu().numpy()
+    out = llm_capi.pa_prefill(_dev(q), _dev(kp), _dev(vp), _dev(pt), row=row, p0=p0,
+                              split=split).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, row, p0)
     assert np.isfinite(out).all()
     assert rel_err(out, ref) < RTOL, rel_err(out, ref)
