@@ -18,8 +18,8 @@
 // (lane l: rows 4(l>>4)+r, column l&15) already holds, per lane, 8 keys of ONE
 // query: that is the B operand of the P·V product once the 32 keys are taken
 // in the k order slot(key) = 8·((key&15)>>2) + 4·(key>>4) + (key&3).  V is
-// staged transposed (Vt[d][slot]) in that same order, so the V^T A operand is
-// one 16-byte LDS read per lane.  The query is the lane's column in both
+// staged row-major and its V^T A operand, in that same key order, is two
+// hardware-transposed LDS reads (ds_read_b64_tr_b16) per 16 dims.  The query is the lane's column in both
 // products, so the running max / sum / rescale are per lane (the 4 lanes of a
 // query agree after a 2-step max exchange).
 //
@@ -62,6 +62,8 @@ struct PaPrefillArgs {
 };
 
 constexpr int kKeyBlock = 32;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
 constexpr float kPScale = 16384.f;  // P enters the PV MFMA as p * 2^14 (hi + lo)
 
 __device__ __forceinline__ void split_f16(float x, _Float16& hi, _Float16& lo) {
@@ -73,7 +75,8 @@ template <int D, int TS, int NW>
 __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
   constexpr int KB = kKeyBlock;
   constexpr int KSTR = D + 8;   // K row stride (halves): conflict-free 16-B row reads
-  constexpr int VSTR = KB + 8;  // V^T row stride (halves): conflict-free 16-B reads
+  constexpr int VSTR = D + 16;  // V row stride (halves): 8·odd dwords, so the
+                                // 64 lanes of a transposed read hit 64 banks
   constexpr int CPR = D / 8;    // 16-byte chunks per key row
   constexpr int NCH = KB * CPR; // chunks per block, each of K and V
   constexpr int NTH = 64 * NW;
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
   constexpr int ND = D / 16;    // 16-dim tiles of the output
   static_assert(NCH % NTH == 0 && D % 32 == 0 && KB % TS == 0, "shape");
   __shared__ __attribute__((aligned(16))) _Float16 Ks[KB * KSTR];
-  __shared__ __attribute__((aligned(16))) _Float16 Vt[D * VSTR];
+  __shared__ __attribute__((aligned(16))) _Float16 Vs[KB * VSTR];
   __shared__ int kval[KB];
 
   const int tid = threadIdx.x;
@@ -140,10 +143,9 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
       ql[kk][e] = lo;
     }
 
-  // Staging: K chunk i of a thread = (key ch / CPR, dims 8 (ch % CPR)) — rows
-  // coalesced; V chunk i = (key ch % KB, dims 8 (ch / KB)) — the 32 keys of a
-  // dim group on adjacent lanes, so the transposed 2-byte LDS writes of a wave
-  // hit distinct slots of one V^T row.
+  // Staging: chunk i of a thread = (key ch / CPR, dims 8 (ch % CPR)) of K and
+  // of V — rows coalesced, both stored row-major ([key][d]); the PV product
+  // reads V transposed with ds_read_b64_tr_b16.
   u32x4 kr[CPT], vr[CPT];
   int vok[CPT];
   auto page_of = [&](int kg) -> int {  // page of key position kg, -1 if none / past lastpos
@@ -155,42 +157,24 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int ch = tid + i * NTH;
-      {
-        const int key = ch / CPR, d0 = (ch % CPR) * 8;
-        const int kg = kb * KB + key;
-        const int pg = page_of(kg);
-        kr[i] = pg >= 0 ? *reinterpret_cast<const u32x4*>(
-                              a.k_pool + (size_t)pg * a.page_stride + ((kg % TS) * D + d0) * 2)
-                        : u32x4{0u, 0u, 0u, 0u};
-      }
-      {
-        const int key = ch % KB, d0 = (ch / KB) * 8;
-        const int kg = kb * KB + key;
-        const int pg = page_of(kg);
-        vok[i] = pg >= 0;
-        // masked keys stage V = 0: a never-written row may hold NaN (0 * NaN)
-        vr[i] = pg >= 0 ? *reinterpret_cast<const u32x4*>(
-                              a.v_pool + (size_t)pg * a.page_stride + ((kg % TS) * D + d0) * 2)
-                        : u32x4{0u, 0u, 0u, 0u};
-      }
+      const int key = ch / CPR, d0 = (ch % CPR) * 8;
+      const int kg = kb * KB + key;
+      const int pg = page_of(kg);
+      const size_t off = (size_t)pg * a.page_stride + ((kg % TS) * D + d0) * 2;
+      vok[i] = pg >= 0;
+      // masked keys stage V = 0: a never-written row may hold NaN (0 * NaN)
+      kr[i] = pg >= 0 ? *reinterpret_cast<const u32x4*>(a.k_pool + off) : u32x4{0u, 0u, 0u, 0u};
+      vr[i] = pg >= 0 ? *reinterpret_cast<const u32x4*>(a.v_pool + off) : u32x4{0u, 0u, 0u, 0u};
     }
   };
   auto stage = [&]() {
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
       const int ch = tid + i * NTH;
-      {
-        const int key = ch / CPR, d0 = (ch % CPR) * 8;
-        *reinterpret_cast<u32x4*>(&Ks[key * KSTR + d0]) = kr[i];
-      }
-      {
-        const int key = ch % KB, d0 = (ch / KB) * 8;
-        const int slot = 8 * ((key & 15) >> 2) + 4 * (key >> 4) + (key & 3);
-        const f16x8 v = __builtin_bit_cast(f16x8, vr[i]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) Vt[(d0 + e) * VSTR + slot] = v[e];
-        if (d0 == 0) kval[key] = vok[i];
-      }
+      const int key = ch / CPR, d0 = (ch % CPR) * 8;
+      *reinterpret_cast<u32x4*>(&Ks[key * KSTR + d0]) = kr[i];
+      *reinterpret_cast<u32x4*>(&Vs[key * VSTR + d0]) = vr[i];
+      if (d0 == 0) kval[key] = vok[i];
     }
   };
 
@@ -250,10 +234,18 @@ __global__ __launch_bounds__(64 * NW) void pa_prefill_kernel(PaPrefillArgs a) {
         pl[4 * t + r] = lo;
       }
     mrun = mnew;
-    // O^T += V^T · P^T
+    // O^T += V^T · P^T.  A operand lane l: V^T[d = 16nd + (l&15)][k 8g+j] =
+    // V[key(8g+j)][d], keys 4g..4g+3 then 16+4g..16+4g+3: two transposed
+    // reads of 4 V rows x 16 columns, lane 4q+p addressing row q, columns 4p..
 #pragma unroll
     for (int nd = 0; nd < ND; ++nd) {
-      const f16x8 vf = *reinterpret_cast<const f16x8*>(&Vt[(16 * nd + c) * VSTR + 8 * g]);
+      const int q4 = c >> 2, p4 = c & 3;
+      const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)&Vs[(4 * g + q4) * VSTR + 16 * nd + 4 * p4]);
+      const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)&Vs[(16 + 4 * g + q4) * VSTR + 16 * nd + 4 * p4]);
+      const f16x8 vf = __builtin_bit_cast(
+          f16x8, s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]});
       O[nd] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, ph, O[nd], 0, 0, 0);
       O[nd] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pl, O[nd], 0, 0, 0);
     }
