@@ -812,6 +812,15 @@ extern "C" size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles,
   return (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
 }
 
+int llm::pa_merge_splits_internal(const float* part_acc, const float* part_ml, float* out,
+                                  const int32_t* context_lens, int B, int H, int D, int T, int TS,
+                                  int pps, int nsplit, int max_tiles, hipStream_t st) {
+  PaMergeArgs mg{part_acc, part_ml, out, context_lens, B, H, D, T, TS, pps, nsplit, max_tiles};
+  hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
+  LLM_HIP_RET(hipGetLastError());
+  return LLM_OK;
+}
+
 int llm::pa_merge_rows_internal(const float* part_acc, const float* part_ml, float* out,
                                 const PaRowOutputs* rows, const int32_t* context_lens, int ctx_p0,
                                 int B, int H, int D, int T, int TS, int pps, int nsplit,
@@ -925,10 +934,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     return pa_merge_rows_internal(a.part_acc, a.part_ml, out, rows, context_lens, -1, B, H, D, T,
                                   TS, pps_fixed, nsplit, kv->max_tiles, st);
   if (!direct) {
-    PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, TS, pps_fixed, nsplit,
-                   kv->max_tiles};
-    hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
-    LLM_HIP_RET(hipGetLastError());
+    const int r = pa_merge_splits_internal(a.part_acc, a.part_ml, out, context_lens, B, H, D, T,
+                                           TS, pps_fixed, nsplit, kv->max_tiles, st);
+    if (r != LLM_OK) return r;
   }
   if (row_out) {  // single split: out is final; convert it in a row pass
     if (rows->q)

@@ -36,6 +36,10 @@ int pa_merge_rows_internal(const float* part_acc, const float* part_ml, float* o
                            int B, int H, int D, int T, int TS, int pps, int nsplit, int max_tiles,
                            hipStream_t st);
 
+int pa_merge_splits_internal(const float* part_acc, const float* part_ml, float* out,
+                             const int32_t* context_lens, int B, int H, int D, int T, int TS,
+                             int pps, int nsplit, int max_tiles, hipStream_t st);
+
 // Causal MFMA attention of a prompt chunk (csrc/pa_prefill.hip, C entry
 // pa_prefill): out rows i < m = attention of query i (position p0 + i) over
 // positions 0 .. p0 + i of page-table row `row`.

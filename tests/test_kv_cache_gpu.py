@@ -150,17 +150,19 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
     assert kv2.free_pages() == kv.free_pages()
 
 
-def test_grouped_attention_shared_prefix_random(gpu, oracle):
+@pytest.mark.parametrize("D,ts,missing", [(64, 16, False), (128, 32, True), (128, 16, True)])
+def test_grouped_attention_shared_prefix_random(gpu, oracle, D, ts, missing):
     """Beam-aware pa_decode_grouped on 3 sequences x 4 beams sharing a prefix
     of pages (the page table rows of a sequence's beams alias the same page
-    ids), ragged per-row contexts: equal to the oracle and to pa_decode."""
+    ids), ragged per-row contexts, optionally missing pages (shared and
+    private): equal to the oracle and to pa_decode."""
     import torch
     import llm_capi
-    rng = np.random.default_rng(8)
-    seqs, W, H, D, ts, T = 3, 4, 4, 64, 16, 700
+    rng = np.random.default_rng(8 + D + ts)
+    seqs, W, H, T = 3, 4, 4, 700
     B = seqs * W
     nt = (T + ts - 1) // ts
-    shared = 30  # tiles shared by the beams of a sequence
+    shared = 30 * 16 // ts  # tiles shared by the beams of a sequence
     num_pages = seqs * H * shared + B * H * (nt - shared) + 3
     perm = rng.permutation(num_pages).astype(np.int32)
     pt = np.full((B, H, nt), -1, np.int32)
@@ -173,6 +175,10 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle):
     for b in range(B):
         pt[b, :, shared:] = perm[i:i + H * (nt - shared)].reshape(H, nt - shared)
         i += H * (nt - shared)
+    if missing:  # a shared tile (all 4 beams) and scattered private tiles
+        pt[0:W, 1, 3] = -1
+        pt[5, 2, shared + 1] = -1
+        pt[9, 0, nt - 2] = -1
     kp = (rng.standard_normal((num_pages, ts, D)) * D ** -0.25).astype(np.float16)
     vp = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
     q = (rng.standard_normal((B, H, D)) * D ** -0.25).astype(np.float32)
@@ -191,6 +197,7 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle):
             outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
                                       row_group=g).cpu().numpy()
             np.testing.assert_array_equal(outg, plain)
+            assert rel_err(outg, ref) < 1e-3
 
 
 @pytest.mark.parametrize("dtype", ["bfloat16", "float32", "int8"])
