@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Driver for GEMM counters: the C3 INT8 decoder (24 L / 16 H / D 128, 64 rows)
+stepped eagerly (LLM_GRAPH=0, so every kernel is its own dispatch) at a short
+context — the weight GEMMs are the same launches as in the 8192-token bench.
+Used under rocprofv3 by scripts/gpu_gemm_pmc.sh."""
+import os
+import sys
+from pathlib import Path
+
+os.environ.setdefault("LLM_GRAPH", "0")
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"))
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    import torch
+    import llm_decoder
+    from bench import CONFIGS, make_weights
+    torch.cuda.set_device(0)
+    cfg = CONFIGS["c3"]
+    hid = cfg["H"] * cfg["D"]
+    dec = llm_decoder.INT8Decoder(cfg["L"], cfg["H"], cfg["D"], hid, cfg["V"], 512,
+                                  max_batch=cfg["B"], page_size=cfg["ts"])
+    dec.set_weights(make_weights(cfg, 1234))
+    dec.begin_synthetic(cfg["B"], 256, 1, True)
+    for i in range(int(os.environ.get("PROF_STEPS", "3"))):
+        dec.step(list(range(cfg["B"])) if i == 0 else None, want_next=False)
+    dec.sync()
+
+
+if __name__ == "__main__":
+    main()
