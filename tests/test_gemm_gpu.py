@@ -20,6 +20,8 @@ def _dev(a):
 @pytest.mark.parametrize("M,K,N", [
     (1, 256, 1024), (16, 768, 2304), (64, 2048, 6144), (64, 8192, 2048), (37, 256, 48),
     (130, 512, 256), (64, 256, 16), (5, 64, 32),
+    # prefill-chunk row counts (M up to 512)
+    (512, 2048, 2048), (300, 512, 256), (256, 8192, 512), (513, 1024, 96),
 ])
 def test_i8_gemm_exact(gpu, oracle, M, K, N):
     import llm_capi
@@ -55,6 +57,7 @@ def test_i8_gemm_no_scales(gpu, oracle):
 @pytest.mark.parametrize("M,K,N,nt,waves", [
     (64, 2048, 6144, 2, 8), (64, 8192, 2048, 1, 8), (64, 2048, 2048, 1, 16), (37, 512, 96, 2, 8),
     (16, 256, 64, 1, 8), (100, 1024, 512, 2, 16),
+    (512, 1024, 768, 0, 0), (300, 512, 4096, 0, 0),  # prefill-chunk row counts
 ])
 def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
     """The decoder's GEMM form: A in packed-A (MFMA fragment) order, forced
@@ -86,7 +89,8 @@ def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
             np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
 
 
-@pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (64, 2048, 512), (3, 96, 48), (80, 256, 64)])
+@pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (64, 2048, 512), (3, 96, 48), (80, 256, 64),
+                                   (512, 768, 2304), (300, 256, 64)])
 def test_f16_gemm(gpu, M, K, N):
     import llm_capi
     rng = np.random.default_rng(K + N)
