@@ -222,6 +222,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many rows in total, sharded over the ranks "
+                         "(default: the config's batch on every rank, weak scaling)")
     ap.add_argument("--seed", type=int, default=1234)
     args = ap.parse_args()
 
@@ -245,6 +248,11 @@ def main():
 
     cfg = CONFIGS[args.config]
     B, T = cfg["B"], cfg["T"]
+    strong = args.global_batch > 0 and "beams" not in cfg
+    if strong:  # rows of this rank
+        if args.global_batch % world:  # the logits gather takes equal shards
+            raise SystemExit(f"--global-batch {args.global_batch} must be a multiple of {world}")
+        B = args.global_batch // world
     hid = cfg["H"] * cfg["D"]
     max_seq = T + args.warmup + args.steps + 8
     cls = getattr(llm_decoder, cfg["cls"])
@@ -310,7 +318,7 @@ def main():
         elapsed = float(t.item())
     t_step = elapsed / args.steps
     T_mean = T + args.warmup + args.steps / 2.0
-    value = B * world / t_step
+    value = (args.global_batch if strong else B * world) / t_step
 
     # roofline of the dominant kernel (paged attention), timed live
     T_now = dec.context_len(0)
@@ -352,12 +360,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int8 GEMM (i32 acc) + fp16 KV attention (fp32 acc)"
             if cfg["cls"] == "INT8Decoder" else "fp16 GEMM + fp16 KV attention (fp32 acc)",
             "data": "synthetic (random-init weights, random fp16 KV context, shuffled pages)",
-            "config": {"workload": cfg["workload"], "global_batch": B * world,
+            "config": {"workload": cfg["workload"] + (f"; strong scaling: {args.global_batch} rows "
+                                                      f"over {world} GPU(s)" if strong else ""),
+                       "global_batch": args.global_batch if strong else B * world,
                        "batch_per_gpu": B, "seq_len": T, "page_size": cfg["ts"],
                        "parallelism": f"batch-sharded x{world} (RCCL logits gather to rank 0)"
                        if not host_gather else f"batch-sharded x{world} ({backend} rehearsal)"},
