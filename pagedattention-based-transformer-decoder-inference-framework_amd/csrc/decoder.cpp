@@ -420,9 +420,11 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
     return pa_prefill_internal(&view, R.q, hid, R.o, hid, R.prefill_row, R.prefill_p0, R.n,
                                cfg.attn_scale, R.attn_ws, R.attn_ws_bytes, st, &ro);
   }
-  // the split merge also produces the o_proj input (packed int8 + scale, or fp16)
+  // the split merge also produces the o_proj input (packed int8 + scale, or fp16);
+  // the fp32 rows are only needed by a single-split (direct) launch
   PaRowOutputs ro;
   ro.pack = 1;
+  ro.keep_out = 0;
   if (wdtype == LLM_I8) {
     ro.q = static_cast<int8_t*>(R.act);
     ro.inv_scale = R.sa;

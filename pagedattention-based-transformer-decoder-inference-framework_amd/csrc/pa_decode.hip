@@ -931,8 +931,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
   if (row_out && !direct)
-    return pa_merge_rows_internal(a.part_acc, a.part_ml, out, rows, context_lens, -1, B, H, D, T,
-                                  TS, pps_fixed, nsplit, kv->max_tiles, st);
+    return pa_merge_rows_internal(a.part_acc, a.part_ml, rows->keep_out ? out : nullptr, rows,
+                                  context_lens, -1, B, H, D, T, TS, pps_fixed, nsplit,
+                                  kv->max_tiles, st);
   if (!direct) {
     const int r = pa_merge_splits_internal(a.part_acc, a.part_ml, out, context_lens, B, H, D, T,
                                            TS, pps_fixed, nsplit, kv->max_tiles, st);

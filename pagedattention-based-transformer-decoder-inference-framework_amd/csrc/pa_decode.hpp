@@ -16,6 +16,7 @@ struct PaRowOutputs {
   float* inv_scale = nullptr;
   void* out16 = nullptr;
   int pack = 0;  // q / out16 in packed-A order (common.hpp a_frag_off_*)
+  int keep_out = 1;  // 0: a split launch skips the fp32 `out` rows (only q / out16 are read)
 };
 
 // `out` (fp32) may be NULL when `rows` requests an output and the launch splits.
