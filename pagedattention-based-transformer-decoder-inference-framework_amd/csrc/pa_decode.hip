@@ -129,7 +129,7 @@ constexpr int kKvLoadAux = 2;
 // of the split (beam-private pages) takes the per-wave direct path.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
-          int KVT = LLM_F16>
+          int KVT = LLM_F16, bool FULLPATH = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
   constexpr int ES = kv_elem_bytes<KVT>();
@@ -255,12 +255,11 @@ void pa_split_kernel(PaSplitArgs a) {
       acc[0] += (float)(x & 1u);
       return;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = p0 + u;
-      const int pg = page_of(min(j, kMaxPps - 1));
-      const bool ok = (j < count) && (pg >= 0);
-      const int tok_base = (tile0 + j) * TS + g;
+    // One page u of the chunk.  FULL (wave-uniform): the page is present and
+    // every one of its tokens is inside the context, so no token needs the
+    // validity selects (the common case: all but a row's last page).
+    auto page_math = [&](auto full_tag, int u, bool ok, int tok_base) {
+      constexpr bool FULL = decltype(full_tag)::value;
       float sc[NI];
       bool valid[NI];
       float mloc = kNegSentinel;
@@ -270,7 +269,7 @@ void pa_split_kernel(PaSplitArgs a) {
 #pragma unroll
         for (int e = 0; e < EPL; ++e) d = fmaf(qv[e], kv_at<KVT>(kk[u * NI + i], e), d);
         d = group_sum<LPT>(d);
-        valid[i] = ok && (tok_base + i * TPI) < Tb;
+        valid[i] = FULL || (ok && (tok_base + i * TPI) < Tb);
         sc[i] = valid[i] ? d : kNegSentinel;
         mloc = fmaxf(mloc, sc[i]);
       }
@@ -285,11 +284,22 @@ void pa_split_kernel(PaSplitArgs a) {
         l += p;
         // Rows past the context (or of a missing page) may hold stale bits, even
         // NaN/Inf in a never-written page: select them away (0 * NaN = NaN).
-        const u32x4 vraw = valid[i] ? vv[u * NI + i] : u32x4{0u, 0u, 0u, 0u};
+        const u32x4 vraw = FULL || valid[i] ? vv[u * NI + i] : u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int e = 0; e < EPL; ++e) acc[e] = fmaf(p, kv_at<KVT>(vraw, e), acc[e]);
       }
       m = mnew;
+    };
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = p0 + u;
+      const int pg = page_of(min(j, kMaxPps - 1));
+      const bool ok = (j < count) && (pg >= 0);
+      const int tok_base = (tile0 + j) * TS + g;
+      if (FULLPATH && ok && (tile0 + j + 1) * TS <= Tb)
+        page_math(std::true_type{}, u, ok, tok_base);
+      else
+        page_math(std::false_type{}, u, ok, tok_base);
     }
   };
 
@@ -1009,6 +1019,8 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
     case 10: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 2, 0, true>), grid, block, 0, st, a); break;
     case 11: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, 2, 1, 8, true>), grid, block, 0, st, a); break;
     case 12: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 2, 2, 0, true>), grid, block, 0, st, a); break;
+    // 13: variant 1 without the full-page fast path (every token takes the validity selects)
+    case 13: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 2, 0, false, false, LLM_F16, false>), grid, block, 0, st, a); break;
     default: return fail(LLM_ERR_INVALID, "pa_decode_tune: variant");
   }
   LLM_HIP_RET(hipGetLastError());
