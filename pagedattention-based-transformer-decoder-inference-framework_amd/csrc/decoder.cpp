@@ -411,6 +411,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
     // the o_proj input conversion the decode merge would have fused
     PaRowOutputs ro;
     ro.pack = 1;
+    ro.keep_out = 0;
     if (wdtype == LLM_I8) {
       ro.q = static_cast<int8_t*>(R.act);
       ro.inv_scale = R.sa;

@@ -379,8 +379,9 @@ int pa_prefill_internal(const pa_kv_view* kv, const float* q, int q_stride, floa
     e = TS == 16 ? launch_prefill<128, 16>(a, pl.nw, st) : launch_prefill<128, 32>(a, pl.nw, st);
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_prefill launch: ") + hipGetErrorString(e));
   if (split)
-    return pa_merge_rows_internal(a.part_acc, a.part_ml, out, rows, nullptr, p0, m, H, D,
-                                  p0 + m, TS, pl.pps, pl.nsplit, kv->max_tiles, st);
+    return pa_merge_rows_internal(a.part_acc, a.part_ml, (rows && !rows->keep_out) ? nullptr : out,
+                                  rows, nullptr, p0, m, H, D, p0 + m, TS, pl.pps, pl.nsplit,
+                                  kv->max_tiles, st);
   if (row_out) {  // one pass: convert the fp32 rows into the o_proj input
     if (rows->q)
       LLM_HIP_RET(launch_quantize_rows(out, m, hid, rows->q, rows->inv_scale, st, rows->pack));

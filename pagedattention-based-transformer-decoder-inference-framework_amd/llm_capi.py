@@ -12,6 +12,7 @@ There is no fallback: if the HIP library is missing, load() raises.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
@@ -123,7 +124,8 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # LLM_CAPI_LIB: another build of the same library (same-box A/B of build flags)
+    p = Path(path) if path else Path(os.environ.get("LLM_CAPI_LIB", LIB_PATH))
     if not p.exists():
         raise FileNotFoundError(
             f"{p} not found: build it with `make -C {HERE}` (or __graft_entry__.build())")

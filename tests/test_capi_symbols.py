@@ -83,6 +83,17 @@ def test_invalid_arguments_rejected_before_any_launch():
     big = exargs[:7] + (8193,)
     assert lib.pa_decode_ex(ctypes.byref(fake), *big, ctypes.byref(opt), None, 0,
                             None) == llm_capi.LLM_ERR_UNSUPPORTED
+    # pa_prefill: NULL view / q / out, unsupported pools (int8) and positions
+    # past the page table are rejected on the host
+    assert lib.pa_prefill(None, None, 0, None, 0, 0, 0, 1, 1.0, None, 0, None) == 1
+    fake.kv_dtype, fake.head_dim, fake.max_tiles = llm_capi.LLM_I8, 128, 4
+    pf = (ctypes.c_void_p(16), 0, ctypes.c_void_p(16), 0, 0, 0, 8, 1.0, None, 0, None)
+    assert lib.pa_prefill(ctypes.byref(fake), *pf) == llm_capi.LLM_ERR_UNSUPPORTED
+    fake.kv_dtype = llm_capi.LLM_F16
+    pf_late = pf[:5] + (100,) + pf[6:]  # positions 100..107 need 7 tiles > max_tiles 4
+    assert lib.pa_prefill(ctypes.byref(fake), *pf_late) == llm_capi.LLM_ERR_INVALID
+    assert b"max_tiles" in lib.llm_last_error()
+    assert lib.pa_prefill_workspace_bytes(ctypes.byref(fake), 0, 0) == 0
     # zero-size work is a successful no-op
     assert lib.pa_decode(ctypes.byref(v), None, None, None, None, 0, 1, 64, 1, 1.0, 0, None, 0,
                          None) == 0
