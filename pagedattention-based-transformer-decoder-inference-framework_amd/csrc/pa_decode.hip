@@ -674,8 +674,16 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
   }
   constexpr int ST = split_stages<D, TS, LLM_F16>();
   if (a.group == 4 && !direct && !lean && ST == 2) {
-    hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, 2, 0, false, true>), grid,
-                       block, 0, st, a);
+    // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
+    // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
+    // 20 % parked (SQ PMC, scripts/gpu_sq_pmc.sh); same-box A/B of the C4
+    // launch: 72-74 vs 76 us (scripts/ab_attention_lib.py, -DLLM_BEAM_CHUNK=)
+#ifndef LLM_BEAM_CHUNK
+#define LLM_BEAM_CHUNK 8192
+#define LLM_BEAM_WAVES 0
+#endif
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
+                                        false, true>), grid, block, 0, st, a);
   } else if (lean && TS * D * 2 <= 4096) {
     // the 8-waves-per-SIMD register budget holds one stage of pages <= 4 KiB
     if constexpr (TS * D * 2 <= 4096) {

@@ -60,8 +60,14 @@ def main():
         i += H * (nt4 - shared)
     q4 = torch.randn((B4, H, D), generator=g, device="cuda") * D ** -0.25
     c4 = timed(lambda: llm_capi.pa_decode(q4, kv4[:-1], kv4[1:], pt4, T=T4, row_group=4))
+    # the first C4 timing also pays first-touch costs; time the default again
+    extra = {"c4_grouped_again_us": round(timed(lambda: llm_capi.pa_decode(
+        q4, kv4[:-1], kv4[1:], pt4, T=T4, row_group=4)), 1)}
+    for pps in [int(x) for x in os.environ.get("AB_C4_PPS", "").split(",") if x]:
+        extra[f"c4_grouped_pps{pps}_us"] = round(timed(lambda: llm_capi.pa_decode(
+            q4, kv4[:-1], kv4[1:], pt4, T=T4, row_group=4, pages_per_split=pps)), 1)
     print(json.dumps({"lib": os.environ.get("LLM_CAPI_LIB", "default"), "c3_us": round(c3, 1),
-                      "c4_grouped_us": round(c4, 1)}), flush=True)
+                      "c4_grouped_us": round(c4, 1)} | extra), flush=True)
 
 
 if __name__ == "__main__":
