@@ -99,8 +99,13 @@ int pa_decode(const pa_kv_view* kv, const float* q, float* out, const int32_t* b
  * README.md:64): rows are taken in groups of row_group (1..4, e.g. the beams of
  * one sequence, rows g*row_group .. g*row_group+row_group-1); the group's rows
  * for one (head, split) run as adjacent waves of one workgroup, so KV pages
- * they share through kv_cache_fork are read from HBM once and re-served from
- * L2.  Results are identical to pa_decode. */
+ * they share through kv_cache_fork are read from HBM once (row_group 4: staged
+ * through LDS, with split boundaries placed by cost so the splits holding the
+ * beam-private tail are not the slowest).  Results equal pa_decode bit for
+ * bit, except for groups of 4 equal-context rows under dynamic splits
+ * (pages_per_split 0), whose cost-balanced partition changes only the fp32
+ * rounding of the split merge.  The workspace is sized by
+ * pa_decode_workspace_bytes as for pa_decode. */
 int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
                       const int32_t* context_lens, int B, int H, int D, int T, float sm_scale,
                       int pages_per_split, int row_group, void* workspace,

@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <cstdlib>
 
 namespace llm {
 
@@ -65,6 +66,8 @@ struct PaSplitArgs {
                // run as adjacent waves of one workgroup, so pages the rows share (a
                // forked prefix) are fetched from HBM once and re-served from L2
   float qscale;
+  int balance16;  // BEAM, dynamic splits: cost of a beam-private tile in 1/16ths of a
+                  // shared tile (>= 16) for cost-balanced split boundaries; 0: off
 };
 
 constexpr int kMaxPps = 128;  // page ids held in two registers per lane
@@ -155,6 +158,7 @@ void pa_split_kernel(PaSplitArgs a) {
   // page-table row and hold the same context (a uniform decision: every wave
   // of the workgroup evaluates the same 4 rows, before any early return).
   bool share = false;
+  int grow[4] = {0, 0, 0, 0};  // BEAM: the group's page-table rows
   if constexpr (BEAM) {
     share = true;
     const int g0 = b - gi;
@@ -168,6 +172,7 @@ void pa_split_kernel(PaSplitArgs a) {
       Ti = min(max(Ti, 0), a.T);
       if (ri < 0 || ri >= a.num_beams || (i > 0 && Ti != T0)) { share = false; break; }
       T0 = Ti;
+      grow[i] = ri;
     }
   }
   if (b >= a.B) return;
@@ -177,13 +182,78 @@ void pa_split_kernel(PaSplitArgs a) {
   int Tb = a.context_lens ? a.context_lens[b] : a.T;
   Tb = min(max(Tb, 0), a.T);
   const int ntiles = min((Tb + TS - 1) / TS, a.max_tiles);
-  const int pps = row_pps(a.pps, a.nsplit, ntiles);
-  const int tile0 = s * pps;
-  const int count = min(pps, ntiles - tile0);
+  int tile0, count;
+  {
+    const int pps = row_pps(a.pps, a.nsplit, ntiles);
+    tile0 = s * pps;
+    count = min(pps, ntiles - tile0);
+  }
+  if constexpr (BEAM) {
+    // Cost-balanced splits: a split's beam-private tiles are loaded by every
+    // wave (4x the per-wave bytes of a shared tile, which the workgroup loads
+    // once), so equal tile counts leave the splits holding the private tail
+    // slowest.  The group's shared prefix (leading tiles whose page ids agree
+    // in all 4 rows) is found cooperatively, 64 tiles per round, and the
+    // boundaries put equal cost (shared 16, private balance16) in each split.
+    // Every input is uniform over the workgroup, so all splits of a row (one
+    // workgroup each) derive the same partition.
+    if (share && a.balance16 >= 16 && a.pps == 0 && a.nsplit > 1 && ntiles > 0) {
+      __shared__ int pfx_lds[4][64];
+      const int32_t* prow = a.page_table + ((size_t)grow[gi] * a.H + h) * a.max_tiles;
+      int nsh_t = 0;
+      for (int blk = 0;; blk += 64) {
+        const int t = blk + lane;
+        int id = -1;
+        if (t < ntiles) {
+          id = prow[t];
+          if (id >= a.num_pages) id = -1;
+        }
+        pfx_lds[gi][lane] = id;
+        __syncthreads();
+        const bool eq = t < ntiles && pfx_lds[0][lane] == pfx_lds[1][lane] &&
+                        pfx_lds[0][lane] == pfx_lds[2][lane] && pfx_lds[0][lane] == pfx_lds[3][lane];
+        const uint64_t mk = __ballot(eq);
+        __syncthreads();
+        const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
+        nsh_t = blk + run;
+        if (run < 64 || blk + 64 >= ntiles) break;
+      }
+      nsh_t = min(nsh_t, ntiles);
+      if (nsh_t > 0 && nsh_t < ntiles) {
+        const long long A = 16, P = a.balance16, ns = a.nsplit;
+        const long long C = A * nsh_t + P * (ntiles - nsh_t);
+        auto start = [&](int k) -> int {  // first tile of split k
+          if (k <= 0) return 0;
+          if (k >= ns) return ntiles;
+          const long long x = (C * k + ns - 1) / ns;
+          if (x <= A * nsh_t) return (int)((x + A - 1) / A);
+          return (int)min<long long>(ntiles, nsh_t + (x - A * nsh_t + P - 1) / P);
+        };
+        // every tile costs >= A, so no split holds more than C/ns/A + 2 tiles
+        if ((C + ns - 1) / ns / A + 2 <= kMaxPps) {
+          tile0 = start(s);
+          count = start(s + 1) - tile0;
+        }
+      }
+    }
+  }
   const int c = lane % LPT;
   const int g = lane / LPT;
 
   if (count <= 0) {
+    if constexpr (BEAM && !DIRECT) {
+      // the merge of a beam launch reads every split: an empty one holds
+      // (m, l, acc) = (sentinel, 0, 0)
+      if (lane < LPT) {
+        float* o = a.part_acc + pidx * D + c * EPL;
+#pragma unroll
+        for (int e = 0; e < EPL; e += 4) *reinterpret_cast<f32x4*>(o + e) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      if (lane == 0) {
+        a.part_ml[pidx * 2] = kNegSentinel;
+        a.part_ml[pidx * 2 + 1] = 0.f;
+      }
+    }
     if constexpr (DIRECT) {
       if (lane < LPT) {
         float* o = a.out + (size_t)bh * D + c * EPL;
@@ -472,7 +542,8 @@ __global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
   Tb = min(max(Tb, 0), a.T);
   const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
   const int pps = row_pps(a.pps, a.nsplit, ntiles);
-  const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
+  // pps < 0: every split holds a partial (beam launches: cost-balanced splits)
+  const int ns = a.pps < 0 ? a.nsplit : min(a.nsplit, (ntiles + pps - 1) / pps);
   const float* ml = a.part_ml + (size_t)bh * a.nsplit * 2;
   float M = kNegSentinel;
   for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
@@ -528,7 +599,8 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   Tb = min(max(Tb, 0), a.T);
   const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
   const int pps = row_pps(a.pps, a.nsplit, ntiles);
-  const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
+  // pps < 0: every split holds a partial (beam launches: cost-balanced splits)
+  const int ns = a.pps < 0 ? a.nsplit : min(a.nsplit, (ntiles + pps - 1) / pps);
   for (int h = w; h < a.H; h += nw) {
     const size_t bh = (size_t)b * a.H + h;
     const float* ml = a.part_ml + bh * a.nsplit * 2;
@@ -658,7 +730,8 @@ long long resident_waves() {
 // vs 1), used when the launch must leave CU room for kernels running beside
 // it (micro-batch overlap).
 template <int D, int TS, int KVT>
-hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_t st) {
+hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_t st,
+                        bool* beam) {
   const int waves = ((a.B + a.group - 1) / a.group) * a.group * a.H * a.nsplit;
   const dim3 grid((waves + 3) / 4), block(256);
   if constexpr (KVT != LLM_F16) {
@@ -684,6 +757,7 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
 #endif
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
                                         false, true>), grid, block, 0, st, a);
+    *beam = true;
   } else if (lean && TS * D * 2 <= 4096) {
     // the 8-waves-per-SIMD register budget holds one stage of pages <= 4 KiB
     if constexpr (TS * D * 2 <= 4096) {
@@ -701,24 +775,25 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
 }
 
 template <int D, int KVT>
-hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, bool lean, hipStream_t st) {
+hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, bool lean, hipStream_t st,
+                       bool* beam) {
   constexpr int ES = kv_elem_bytes<KVT>();
   if (TS == 16) {
-    if constexpr (kv_shape_ok(D, 16, ES)) return launch_split<D, 16, KVT>(a, direct, lean, st);
+    if constexpr (kv_shape_ok(D, 16, ES)) return launch_split<D, 16, KVT>(a, direct, lean, st, beam);
   } else if (TS == 32) {
-    if constexpr (kv_shape_ok(D, 32, ES)) return launch_split<D, 32, KVT>(a, direct, lean, st);
+    if constexpr (kv_shape_ok(D, 32, ES)) return launch_split<D, 32, KVT>(a, direct, lean, st, beam);
   }
   return hipErrorInvalidValue;
 }
 
 template <int D>
 hipError_t dispatch_kvt(const PaSplitArgs& a, int kvt, int TS, bool direct, bool lean,
-                        hipStream_t st) {
+                        hipStream_t st, bool* beam) {
   switch (kvt) {
-    case LLM_F16: return dispatch_ts<D, LLM_F16>(a, TS, direct, lean, st);
-    case LLM_BF16: return dispatch_ts<D, LLM_BF16>(a, TS, direct, lean, st);
-    case LLM_F32: return dispatch_ts<D, LLM_F32>(a, TS, direct, lean, st);
-    case LLM_I8: return dispatch_ts<D, LLM_I8>(a, TS, direct, lean, st);
+    case LLM_F16: return dispatch_ts<D, LLM_F16>(a, TS, direct, lean, st, beam);
+    case LLM_BF16: return dispatch_ts<D, LLM_BF16>(a, TS, direct, lean, st, beam);
+    case LLM_F32: return dispatch_ts<D, LLM_F32>(a, TS, direct, lean, st, beam);
+    case LLM_I8: return dispatch_ts<D, LLM_I8>(a, TS, direct, lean, st, beam);
     default: return hipErrorInvalidValue;
   }
 }
@@ -859,6 +934,58 @@ int llm::pa_merge_rows_internal(const float* part_acc, const float* part_ml, flo
   return LLM_OK;
 }
 
+namespace {
+// Cost of a beam-private tile relative to a shared one, in 1/16ths (beam-group
+// launches, dynamic splits).  LLM_BEAM_BALANCE16 overrides it (0: equal tile
+// counts, the plain partition) for tuning.
+int beam_balance16() {
+  static const int v = [] {
+    const char* e = std::getenv("LLM_BEAM_BALANCE16");
+    const int x = e ? std::atoi(e) : 44;
+    return x >= 16 ? x : 0;
+  }();
+  return v;
+}
+
+// Resident waves of the beam-group kernel (0 where the plain schedule runs
+// instead: pages above 8 KiB).
+template <int D, int TS>
+long long beam_resident_waves() {
+  if constexpr (!kv_shape_ok(D, TS, 2) || split_stages<D, TS, LLM_F16>() != 2) {
+    return 0;
+  } else {
+    static long long cached = -1;
+    if (cached >= 0) return cached;
+    int dev = 0, cus = 0, blocks = 0;
+    cached = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &blocks,
+            pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true>,
+            256, 0) == hipSuccess &&
+        cus > 0 && blocks > 0)
+      cached = (long long)cus * blocks * 4;
+    else
+      (void)hipGetLastError();
+    return cached;
+  }
+}
+
+long long beam_resident_waves_for(int D, int TS) {
+  auto by_ts = [&](auto d) -> long long {
+    constexpr int DD = decltype(d)::value;
+    return TS == 16 ? beam_resident_waves<DD, 16>() : beam_resident_waves<DD, 32>();
+  };
+  switch (D) {
+    case 32: return by_ts(std::integral_constant<int, 32>{});
+    case 64: return by_ts(std::integral_constant<int, 64>{});
+    case 128: return by_ts(std::integral_constant<int, 128>{});
+    default: return by_ts(std::integral_constant<int, 256>{});
+  }
+}
+}  // namespace
+
 int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                             int D, int T, float sm_scale, int pages_per_split, void* workspace,
@@ -909,6 +1036,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
       resident = resident_waves_for(D, TS, kv->kv_dtype);
     }
   }
+  // beam-group launches size their splits for the beam kernel's occupancy
+  // (4 waves per SIMD against the plain kernel's 2: C4 8 splits, not 4)
+  if (pps_fixed <= 0 && !lean && row_group == 4 && kv->kv_dtype == LLM_F16)
+    resident = std::max(resident, beam_resident_waves_for(D, TS));
   const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
   const bool direct = nsplit <= 1;
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
@@ -940,21 +1071,23 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     a.part_acc = static_cast<float*>(workspace);
     a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   }
+  a.balance16 = beam_balance16();
   hipError_t e;
+  bool beam = false;  // the beam kernel ran: every split holds a partial
   switch (D) {
-    case 32: e = dispatch_kvt<32>(a, kv->kv_dtype, TS, direct, lean, st); break;
-    case 64: e = dispatch_kvt<64>(a, kv->kv_dtype, TS, direct, lean, st); break;
-    case 128: e = dispatch_kvt<128>(a, kv->kv_dtype, TS, direct, lean, st); break;
-    default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, lean, st); break;
+    case 32: e = dispatch_kvt<32>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
+    case 64: e = dispatch_kvt<64>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
+    case 128: e = dispatch_kvt<128>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
+    default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
   if (row_out && !direct)
     return pa_merge_rows_internal(a.part_acc, a.part_ml, rows->keep_out ? out : nullptr, rows,
-                                  context_lens, -1, B, H, D, T, TS, pps_fixed, nsplit,
+                                  context_lens, -1, B, H, D, T, TS, beam ? -1 : pps_fixed, nsplit,
                                   kv->max_tiles, st);
   if (!direct) {
     const int r = pa_merge_splits_internal(a.part_acc, a.part_ml, out, context_lens, B, H, D, T,
-                                           TS, pps_fixed, nsplit, kv->max_tiles, st);
+                                           TS, beam ? -1 : pps_fixed, nsplit, kv->max_tiles, st);
     if (r != LLM_OK) return r;
   }
   if (row_out) {  // single split: out is final; convert it in a row pass

@@ -42,7 +42,8 @@ def main():
     c3 = timed(lambda: llm_capi.pa_decode(q, kv[:-1], kv[1:], pt, T=T))
     del kv
     # C4 shape: 8 seqs x 4 beams, 240 shared tiles + 16 private per beam
-    S, W, T4, shared = 8, 4, 4096, 240
+    S, W, T4 = 8, 4, 4096
+    shared = int(os.environ.get("AB_C4_SHARED", 240))  # tiles of the forked prefix
     nt4 = T4 // ts
     B4 = S * W
     npages = S * H * shared + B4 * H * (nt4 - shared)
