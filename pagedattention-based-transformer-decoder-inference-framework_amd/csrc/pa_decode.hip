@@ -70,7 +70,8 @@ struct PaSplitArgs {
                   // shared tile (>= 16) for cost-balanced split boundaries; 0: off
 };
 
-constexpr int kMaxPps = 128;  // page ids held in two registers per lane
+constexpr int kMaxPps = 128;     // page ids held in two registers per lane
+constexpr int kMaxSplits = 128;  // split weights held in two registers per merge lane
 
 // Split length of a row with `ntiles` live tiles.
 __device__ __forceinline__ int row_pps(int pps_fixed, int nsplit, int ntiles) {
@@ -820,7 +821,9 @@ long long max_nsplit(int B, int H, int ntiles) {
   const long long bh = std::max(1LL, (long long)B * H);
   const long long cap = 256LL * kMaxWavesPerCu;  // largest resident-wave count
   const long long lo = (ntiles + kMaxPps - 1) / kMaxPps;
-  return std::max(lo, std::min<long long>((ntiles + kMinPps - 1) / kMinPps, lo + (cap + bh - 1) / bh + 1));
+  return std::min<long long>(
+      kMaxSplits,
+      std::max(lo, std::min<long long>((ntiles + kMinPps - 1) / kMinPps, lo + (cap + bh - 1) / bh + 1)));
 }
 
 // Splits per (b, h): the smallest NS that is a whole number of resident-wave
@@ -1041,6 +1044,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   if (pps_fixed <= 0 && !lean && row_group == 4 && kv->kv_dtype == LLM_F16)
     resident = std::max(resident, beam_resident_waves_for(D, TS));
   const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
+  if (nsplit > kMaxSplits || (long long)nsplit * (pps_fixed > 0 ? pps_fixed : kMaxPps) < ntiles_max)
+    return fail(LLM_ERR_UNSUPPORTED,
+                "pa_decode: at most 128 splits of at most 128 pages per row (raise "
+                "pages_per_split, or pass 0; T <= 16384 pages)");
   const bool direct = nsplit <= 1;
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
 
@@ -1129,7 +1136,7 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
   const int ntiles_max = std::max(1, (T + 15) / 16);
   pps = std::min(std::max(pps, 1), kMaxPps);
   const int nsplit = (ntiles_max + pps - 1) / pps;
-  LLM_REQUIRE(nsplit > 1, "pa_decode_tune: needs more than one split");
+  LLM_REQUIRE(nsplit > 1 && nsplit <= kMaxSplits, "pa_decode_tune: needs 2..128 splits");
   const size_t need = (size_t)B * H * nsplit * (128 + 2) * sizeof(float);
   LLM_REQUIRE(workspace && workspace_bytes >= need, "pa_decode_tune: workspace");
   PaSplitArgs a{};

@@ -41,6 +41,9 @@ def test_abi_version_and_pure_host_helpers():
     assert lib.pa_decode_pages_per_split(16, 12, 2048, 16, 128) == 8
     assert lib.pa_decode_workspace_bytes(2, 2, 64, 16, 8) == 2 * 2 * 2 * (64 + 2) * 4
     assert lib.pa_decode_pages_per_split(-1, 1, 1, 16, 1) == -1
+    # few (row, head) pairs over a long context: at most 128 splits (the merge's
+    # two split-weight registers per lane)
+    assert lib.pa_decode_workspace_bytes(1, 1, 64, 2500, 0) == 1 * 1 * 128 * 66 * 4
 
 
 def test_invalid_arguments_rejected_before_any_launch():

@@ -406,3 +406,25 @@ def test_paged_attention_binding_filters(gpu, oracle):
     ref, rp, _ = oracle.paged_attention(q, kp, vp, pt, T=T, top_k=10, top_p=0.9, want_probs=True)
     assert rel_err(out.cpu().numpy(), ref) < RTOL
     np.testing.assert_array_equal(probs.cpu().numpy() > 0, rp > 0)
+
+
+@pytest.mark.parametrize("B,H", [(1, 1), (1, 8)])
+def test_pa_decode_long_context_few_rows(gpu, oracle, B, H):
+    """A long context on few (row, head) pairs wants many splits: they are
+    capped at 128 (the merge keeps 128 split weights per lane) with pages per
+    split raised to match.  T = 40000 is 2500 pages: 128 splits of <= 20.
+    A fixed pages_per_split that would need more than 128 splits is rejected."""
+    import llm_capi
+    rng = np.random.default_rng(B * 10 + H)
+    D, ts, T = 64, 16, 40000
+    nt = (T + ts - 1) // ts
+    num_pages = B * H * nt
+    kp = (rng.standard_normal((num_pages, ts, D)) * D ** -0.25).astype(np.float16)
+    vp = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
+    pt = rng.permutation(num_pages).astype(np.int32).reshape(B, H, nt)
+    q = (rng.standard_normal((B, H, D)) * D ** -0.25).astype(np.float32)
+    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T)
+    out = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T).cpu().numpy()
+    assert rel_err(out, ref) < RTOL
+    with pytest.raises(llm_capi.LlmError, match="128 splits"):
+        llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=T, pages_per_split=8)
