@@ -38,7 +38,11 @@ def test_abi_version_and_pure_host_helpers():
     assert lib.pa_decode_pages_per_split(64, 16, 8192, 16, 513) == 86
     # dynamic splits: bounded by ceil(513/128) + ceil(8192/1024) + 1 = 14 splits
     assert lib.pa_decode_workspace_bytes(64, 16, 128, 513, 0) == 64 * 16 * 14 * 130 * 4
-    assert lib.pa_decode_pages_per_split(16, 12, 2048, 16, 128) == 32  # short splits merged
+    # small launches: fewer, longer splits (>= 32 pages) while >= 512 waves remain
+    assert lib.pa_decode_pages_per_split(16, 12, 2048, 16, 128) == 32  # C2: 4 splits
+    assert lib.pa_decode_pages_per_split(8, 16, 4096, 16, 256) == 32
+    assert lib.pa_decode_pages_per_split(1, 16, 8192, 16, 512) == 16   # 512 waves
+    assert lib.pa_decode_pages_per_split(4, 12, 1024, 16, 64) == 8     # too few waves
     assert lib.pa_decode_workspace_bytes(2, 2, 64, 16, 8) == 2 * 2 * 2 * (64 + 2) * 4
     assert lib.pa_decode_pages_per_split(-1, 1, 1, 16, 1) == -1
     # few (row, head) pairs over a long context: at most 128 splits (the merge's
