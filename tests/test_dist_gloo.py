@@ -80,9 +80,11 @@ def _worker(rank, world, port, rows, steps, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_shard_and_gather():
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_gloo_shard_and_gather(world):
+    """world 2 (the N > 1 path) and world 4 (ragged shards: 5 rows as 2/1/1/1)."""
     import torch.multiprocessing as mp
-    rows, steps, world = 5, 4, 2
+    rows, steps = 5, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
