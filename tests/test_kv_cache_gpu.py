@@ -154,7 +154,8 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
     assert kv2.free_pages() == kv.free_pages()
 
 
-@pytest.mark.parametrize("D,ts,missing", [(64, 16, False), (128, 32, True), (128, 16, True)])
+@pytest.mark.parametrize("D,ts,missing", [(64, 16, False), (128, 32, True), (128, 16, True),
+                                           (32, 16, True), (256, 16, False), (256, 32, True)])
 def test_grouped_attention_shared_prefix_random(gpu, oracle, D, ts, missing):
     """Beam-aware pa_decode_grouped on 3 sequences x 4 beams sharing a prefix
     of pages (the page table rows of a sequence's beams alias the same page
@@ -211,7 +212,8 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle, D, ts, missing):
 
 @pytest.mark.parametrize("shared", [0, 1, 17, 43, 44])
 @pytest.mark.parametrize("T", [700, 16 * 44 - 5])
-def test_grouped_attention_cost_balanced_splits(gpu, oracle, shared, T):
+@pytest.mark.parametrize("kvt", ["float16", "bfloat16"])
+def test_grouped_attention_cost_balanced_splits(gpu, oracle, shared, T, kvt):
     """Beam groups whose 4 rows share the first `shared` of 44 tiles: the
     beam kernel splits the row by cost (a private tile is loaded per wave, a
     shared tile once per workgroup), and splits may be empty; every shared
@@ -239,16 +241,22 @@ def test_grouped_attention_cost_balanced_splits(gpu, oracle, shared, T):
     vp = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
     q = (rng.standard_normal((B, H, D)) * D ** -0.25).astype(np.float32)
     d = lambda a: torch.from_numpy(a).cuda()
-    ref = oracle.paged_attention(q, kp.astype(np.float32), vp.astype(np.float32), pt, T=T)
-    plain = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T).cpu().numpy()
-    outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, row_group=4).cpu().numpy()
+    # bf16 pools take the standard schedule (no beam kernel): bitwise the plain one
+    kd = d(kp).to(getattr(torch, kvt))
+    vd = d(vp).to(getattr(torch, kvt))
+    kf, vf = kd.float().cpu().numpy(), vd.float().cpu().numpy()
+    ref = oracle.paged_attention(q, kf, vf, pt, T=T)
+    plain = llm_capi.pa_decode(d(q), kd, vd, d(pt), T=T).cpu().numpy()
+    outg = llm_capi.pa_decode(d(q), kd, vd, d(pt), T=T, row_group=4).cpu().numpy()
+    if kvt == "bfloat16":
+        np.testing.assert_array_equal(outg, plain)
     assert rel_err(plain, ref) < 1e-3
     assert rel_err(outg, ref) < 1e-3
     assert rel_err(outg, plain) < 1e-5
     # fixed pages per split keep the uniform partition, empty splits included
-    outf = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, row_group=4,
+    outf = llm_capi.pa_decode(d(q), kd, vd, d(pt), T=T, row_group=4,
                               pages_per_split=24).cpu().numpy()
-    plainf = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T,
+    plainf = llm_capi.pa_decode(d(q), kd, vd, d(pt), T=T,
                                 pages_per_split=24).cpu().numpy()
     np.testing.assert_array_equal(outf, plainf)
 
