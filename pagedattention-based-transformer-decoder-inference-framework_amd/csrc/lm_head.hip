@@ -10,7 +10,7 @@
 // To keep ~fp32 accuracy x is split into fp16 hi + lo and each E fragment
 // feeds two v_mfma_f32_16x16x32_f16.
 //
-// Layout of the work: one workgroup = 8 waves = 128 vocabulary rows of E
+// Layout of the work: one workgroup = 16 waves = 256 vocabulary rows of E
 // (each wave one 16-row tile), all M rows of x.  x is the operand every
 // workgroup shares: it is staged per 256-wide K chunk into LDS once per
 // workgroup (converted to hi/lo A fragments on the way), so the per-CU
@@ -30,7 +30,15 @@
 
 namespace llm {
 
-constexpr int kLmWaves = 8;
+// 16 waves = 256 vocabulary rows per workgroup: x is staged once per 256 rows
+// instead of 128, halving its share of the per-CU traffic (rocprof, C3 shape,
+// scripts/time_lm_head.py: 57.6 vs 73.3 us per launch, identical logits; M 16 /
+// 32 / 64 at K 768-2048: 16.2 vs 16.7, 45.2 vs 47.0, 24.2 vs 32.4 us)
+#ifndef LLM_LM_WAVES
+#define LLM_LM_WAVES 16
+#endif
+constexpr int kLmWaves = LLM_LM_WAVES;
+constexpr int kLmThreads = 64 * kLmWaves;
 constexpr int kLmCols = 16 * kLmWaves;  // vocabulary rows per workgroup
 constexpr int kLmKChunk = 256;          // K per LDS stage (8 k-steps of 32)
 constexpr int kLmKs = kLmKChunk / 32;
@@ -47,7 +55,7 @@ struct LmHeadArgs {
 
 // MT = 16-row tiles of x per workgroup (1, 2 or 4).
 template <int MT>
-__global__ __launch_bounds__(512) void lm_head_kernel(LmHeadArgs a) {
+__global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
   // A fragments of the chunk: [mt][ks][hi/lo][64 lanes] x 16 B
   __shared__ __attribute__((aligned(16))) u32x4 xa[MT][kLmKs][2][64];
   __shared__ float pv[kLmWaves][16 * MT];
@@ -81,14 +89,15 @@ __global__ __launch_bounds__(512) void lm_head_kernel(LmHeadArgs a) {
   // lane l holds row mt*16 + (l&15), k = ks*32 + 8*(l>>4) .. +8.  Each thread
   // owns FPT fragments; chunk c+1's x is loaded into registers while chunk c
   // is multiplied.
-  constexpr int FPT = MT * kLmKs * 64 / 512;  // fragments per thread (1, 2 or 4)
+  constexpr int NFRAG = MT * kLmKs * 64;
+  constexpr int FPT = (NFRAG + kLmThreads - 1) / kLmThreads;  // fragments per thread
   f32x4 xr[FPT][2];
   auto load_x = [&](int c) {
 #pragma unroll
     for (int i = 0; i < FPT; ++i) {
-      const int f = threadIdx.x + i * 512;
+      const int f = threadIdx.x + i * kLmThreads;
       const int l = f & 63, ks = (f >> 6) % kLmKs, mt = (f >> 6) / kLmKs;
-      const int row = m0 + mt * 16 + (l & 15);
+      const int row = f < NFRAG ? m0 + mt * 16 + (l & 15) : a.M;
       const int k = c * kLmKChunk + ks * 32 + 8 * (l >> 4);
       xr[i][0] = xr[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (row < a.M && k < a.K && !(a.mode & 2)) {
@@ -101,7 +110,8 @@ __global__ __launch_bounds__(512) void lm_head_kernel(LmHeadArgs a) {
   auto store_x = [&]() {
 #pragma unroll
     for (int i = 0; i < FPT; ++i) {
-      const int f = threadIdx.x + i * 512;
+      const int f = threadIdx.x + i * kLmThreads;
+      if (f >= NFRAG) break;
       const int l = f & 63, ks = (f >> 6) % kLmKs, mt = (f >> 6) / kLmKs;
       f16x8 hi, lo;
 #pragma unroll
@@ -178,7 +188,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(LmHeadArgs a) {
   }
   if (!a.part_val) return;
   __syncthreads();
-  for (int row = threadIdx.x; row < 16 * MT; row += 512) {
+  for (int row = threadIdx.x; row < 16 * MT; row += kLmThreads) {
     if (m0 + row >= a.M) continue;
     float bv = pv[0][row];
     int bi = pi[0][row];
@@ -261,7 +271,7 @@ hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, i
   LmHeadArgs a{x, static_cast<const _Float16*>(E), logits, part_val, part_idx, M, V, K,
                lm_head_workgroups(V), mode};
   const int mt = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  const dim3 grid(a.nwg, (M + 16 * mt - 1) / (16 * mt)), block(512);
+  const dim3 grid(a.nwg, (M + 16 * mt - 1) / (16 * mt)), block(kLmThreads);
   if (mt == 1) hipLaunchKernelGGL(lm_head_kernel<1>, grid, block, 0, st, a);
   else if (mt == 2) hipLaunchKernelGGL(lm_head_kernel<2>, grid, block, 0, st, a);
   else hipLaunchKernelGGL(lm_head_kernel<4>, grid, block, 0, st, a);
