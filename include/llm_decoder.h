@@ -73,8 +73,11 @@ typedef struct pa_kv_view {
 /* Bytes of device workspace pa_decode needs (split-T partial softmax state). */
 size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles, int pages_per_split);
 
-/* Split-T count heuristic used when pages_per_split <= 0: enough waves to
- * fill 256 CUs.  Returns the pages-per-split pa_decode will use. */
+/* Host-only ESTIMATE of the split-T size pa_decode picks when
+ * pages_per_split <= 0, for a uniform context T: it assumes 3,072 resident
+ * waves (256 CUs x 12) where pa_decode queries the device's occupancy for the
+ * kernel it launches and derives each row's split length from that row's own
+ * context, so the two can differ.  For labelling runs, not for sizing them. */
 int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles);
 
 /* Paged decode attention (replaces paged_flash_attention_kernel_fused,
@@ -269,10 +272,36 @@ void* kv_cache_k_pool(kv_cache* c);
 void* kv_cache_v_pool(kv_cache* c);
 long long kv_cache_page_stride(const kv_cache* c);
 int32_t* kv_cache_page_table(kv_cache* c, int layer);
-/* KVTileCache::save_to_file / load_from_file (kv_tile_cache.cpp:105-125):
- * header + page table + used pages. */
+/* Snapshot of the whole cache ("APPIMKV2": geometry, layered page table, used
+ * pages K then V) — this build's own format, the one that restores the page
+ * table too.  kv_cache_load validates the whole file (geometry, every table
+ * entry and page id in [-1, num_pages), exact size) before it changes the
+ * cache; on a failure after that point the cache is left cleared. */
 int kv_cache_save(const kv_cache* c, const char* path);
 int kv_cache_load(kv_cache* c, const char* path);
+/* Validate a snapshot on the host (no device needed): geometry[9] receives
+ * {L, beams, H, D, page_size, max_tiles, num_pages, kv_dtype, used_pages}. */
+int kv_cache_inspect(const char* path, long long* geometry);
+/* KVTileCache<T>::save_to_file / load_from_file (kv_cache/kv_tile_cache.cpp:
+ * 105-125), byte for byte: the raw K pool [num_pages][page_size][head_dim]
+ * then the raw V pool, no header, no page table (the reader keeps its own).
+ * load_pools refuses a file whose size is not 2 * num_pages * page bytes. */
+int kv_cache_save_pools(const kv_cache* c, const char* path);
+int kv_cache_load_pools(kv_cache* c, const char* path);
+/* KVTileCacheCPU<T>::save / load (kv_cache/kv_tile_cache_cpu.cpp:89-123), byte
+ * for byte: int32 count, then per tile {int32 batch_id, head_id, tile_id} and
+ * page_size * head_dim elements.  One file holds the K (kind 0) or V (kind 1)
+ * tiles of one layer (the reference keeps K and V in two caches); batch_id is
+ * the beam.  save writes every mapped tile in (beam, head, tile) order (the
+ * reference's order is its hash map's).  load maps each record's tile (a new
+ * page, or copy-on-write of a shared one) and writes its data; a later record
+ * of the same tile wins, as in the reference; records outside this cache's
+ * (beam, head, tile) range are refused before anything changes. */
+int kv_cache_save_tiles(const kv_cache* c, int layer, int kind, const char* path);
+int kv_cache_load_tiles(kv_cache* c, int layer, int kind, const char* path);
+/* Validate a tile-record file of tile_bytes-byte tiles on the host (no device
+ * needed); *count receives its record count. */
+int kv_tiles_inspect(const char* path, long long tile_bytes, int* count);
 
 /* ------------------------------------------------------------------------ */
 /* Decoder (CUDADecoder / INT8Decoder, decoder/cuda_decoder.hpp:7-21,        */
@@ -369,6 +398,17 @@ int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_width, int sh
 int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
                      int32_t* next_host, void* stream);
 int llm_decoder_sync(llm_decoder* d);
+/* Activation taps for parity checks (INT8 decoders): every following
+ * llm_decoder_step also copies, per layer l and stage s (0: LN1 output, 1:
+ * attention output, 2: LN2 output, 3: fc1 output -- the four int8 GEMM inputs
+ * of DecoderBlock::forward, decoder/decoder_block.hpp:43-61), the rows' int8
+ * activations in packed-A order (common.hpp a_frag_off_i8) to
+ *   q_dev + ((l*4 + s) * ceil(max_batch/16)*16 + row) * K   (K = hidden_dim, or
+ *                                                           inter_dim at s = 3;
+ *   slot stride ceil(max_batch/16)*16 * max(hidden_dim, inter_dim) bytes)
+ * and their fp32 dequantisation scales to s_dev[(l*4 + s) * max_batch + row].
+ * Both NULL switches the taps off.  Prefill chunks are not tapped. */
+int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev);
 int llm_decoder_context_len(const llm_decoder* d, int row);
 kv_cache* llm_decoder_kv(llm_decoder* d);
 

@@ -404,9 +404,39 @@ uint16_t* oracle_decoder_kv_ptr(void* h, int layer, int which) {
 // One decode step for all B rows.  tokens[b] is the token at position pos[b];
 // attention covers positions [0, pos[b]].  Runs the first `layers_to_run`
 // layers (all if < 0) and the LM head + argmax if do_lm_head.
+//
+// Teacher forcing (oracle_decoder_step_forced): at each of a layer's four int8
+// GEMM inputs (stage 0: LN1 output, 1: attention output, 2: LN2 output, 3: fc1
+// output) the oracle quantises its own fp32 values as usual, compares them with
+// the given activations (forced_q [L][4][B][Kmax] int8, forced_s [L][4][B] fp32
+// scales, Kmax = max(hid, inter)), then continues from the GIVEN ones.  A fp32
+// reduction-order difference can move a value across an int8 rounding boundary
+// (one LSB); forcing keeps such a flip from propagating, so the rest of the
+// step is compared at full precision.  stats [L][4][3]: number of int8 values
+// that differ, their max |difference|, max rel. difference of the scales.
+static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
+                        int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
+                        int32_t* next_out, const int8_t* forced_q, const float* forced_s,
+                        float* stats);
+
 int oracle_decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
                         int32_t* next_out) {
+  return decoder_step(handle, tokens, pos, attn_scale, layers_to_run, do_lm_head, x_out,
+                      logits_out, next_out, nullptr, nullptr, nullptr);
+}
+
+int oracle_decoder_step_forced(void* handle, const int32_t* tokens, const int32_t* pos,
+                               float attn_scale, float* logits_out, int32_t* next_out,
+                               const int8_t* forced_q, const float* forced_s, float* stats) {
+  return decoder_step(handle, tokens, pos, attn_scale, -1, 1, nullptr, logits_out, next_out,
+                      forced_q, forced_s, stats);
+}
+
+static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
+                        int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
+                        int32_t* next_out, const int8_t* forced_q, const float* forced_s,
+                        float* stats) {
   auto* d = static_cast<OracleDecoder*>(handle);
   const oracle_model& m = d->m;
   const int B = d->B, H = m.H, D = m.D, hid = m.hid, inter = m.inter;
@@ -420,10 +450,35 @@ int oracle_decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
   for (int b = 0; b < B; ++b)
     for (int j = 0; j < hid; ++j) x[(size_t)b * hid + j] = half_to_float(m.emb[(size_t)tokens[b] * hid + j]);
 
+  const int Kmax = std::max(hid, inter);
+  // quantise `in` [B][K] into qa / sa, then (teacher forcing) compare with and
+  // take the given activations of (layer, stage)
+  auto quant = [&](int l, int stage, const float* in, int K) {
+    oracle_quantize_rows(in, B, K, qa.data(), sa.data());
+    if (!forced_q) return;
+    const size_t slot = (size_t)l * 4 + stage;
+    float n_diff = 0, max_diff = 0, max_srel = 0;
+    for (int b = 0; b < B; ++b) {
+      const int8_t* fq = forced_q + (slot * B + b) * Kmax;
+      for (int j = 0; j < K; ++j) {
+        const int dq = std::abs((int)qa[(size_t)b * K + j] - (int)fq[j]);
+        if (dq) { n_diff += 1; max_diff = std::max(max_diff, (float)dq); }
+        qa[(size_t)b * K + j] = fq[j];
+      }
+      const float fs = forced_s[slot * B + b];
+      max_srel = std::max(max_srel, std::abs(fs - sa[b]) / std::max(std::abs(sa[b]), 1e-30f));
+      sa[b] = fs;
+    }
+    if (stats) {
+      stats[slot * 3 + 0] = n_diff;
+      stats[slot * 3 + 1] = max_diff;
+      stats[slot * 3 + 2] = max_srel;
+    }
+  };
   for (int l = 0; l < Lrun; ++l) {
     const size_t lh = (size_t)l * hid;
     oracle_layer_norm(x.data(), B, hid, m.ln1_g + lh, m.ln1_b + lh, 1e-5f, a.data());
-    oracle_quantize_rows(a.data(), B, hid, qa.data(), sa.data());
+    quant(l, 0, a.data(), hid);
     oracle_i8_gemm(qa.data(), m.wqkv + (size_t)l * hid * 3 * hid, nullptr, qkv.data(), B, 3 * hid,
                    hid, sa.data(), m.sw_qkv + (size_t)l * 3 * hid, nullptr, 0);
     // KV append (fp16 storage, round to nearest even).
@@ -461,14 +516,14 @@ int oracle_decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
         }
       }
     }
-    oracle_quantize_rows(o.data(), B, hid, qa.data(), sa.data());
+    quant(l, 1, o.data(), hid);
     oracle_i8_gemm(qa.data(), m.wo + (size_t)l * hid * hid, nullptr, x.data(), B, hid, hid,
                    sa.data(), m.sw_o + lh, nullptr, 0);
     oracle_layer_norm(x.data(), B, hid, m.ln2_g + lh, m.ln2_b + lh, 1e-5f, a.data());
-    oracle_quantize_rows(a.data(), B, hid, qa.data(), sa.data());
+    quant(l, 2, a.data(), hid);
     oracle_i8_gemm(qa.data(), m.w1 + (size_t)l * hid * inter, nullptr, h1.data(), B, inter, hid,
                    sa.data(), m.sw1 + (size_t)l * inter, m.b1 + (size_t)l * inter, 1);
-    oracle_quantize_rows(h1.data(), B, inter, qa.data(), sa.data());
+    quant(l, 3, h1.data(), inter);
     oracle_i8_gemm(qa.data(), m.w2 + (size_t)l * inter * hid, nullptr, x.data(), B, hid, inter,
                    sa.data(), m.sw2 + lh, m.b2 + lh, 0);
   }

@@ -87,6 +87,9 @@ class Oracle:
         L.oracle_decoder_step.restype = ctypes.c_int
         L.oracle_decoder_step.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_float,
                                           ctypes.c_int, ctypes.c_int, _f32p, _f32p, _i32p]
+        L.oracle_decoder_step_forced.restype = ctypes.c_int
+        L.oracle_decoder_step_forced.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_float,
+                                                 _f32p, _i32p, _i8p, _f32p, _f32p]
         L.oracle_num_threads.restype = ctypes.c_int
 
     # -- attention ---------------------------------------------------------
@@ -213,6 +216,28 @@ class OracleDecoder:
         arr = np.ctypeslib.as_array(p, shape=(n,)).view(np.float16)
         return arr.reshape(self.B, c["H"], c["max_seq"], c["D"])
 
+    def step_forced(self, tokens, pos, forced_q, forced_s, attn_scale=1.0):
+        """One step teacher-forced at every int8 GEMM input (oracle.cpp
+        oracle_decoder_step_forced): forced_q [L][4][B][max(hid, inter)] int8,
+        forced_s [L][4][B] fp32.  Returns (logits, next, stats [L][4][3]: int8
+        values that differed from the oracle's own quantisation, their max
+        |difference|, max rel. difference of the row scales)."""
+        c = self.cfg
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        pos = np.ascontiguousarray(pos, np.int32)
+        fq = np.ascontiguousarray(forced_q, np.int8)
+        fs = np.ascontiguousarray(forced_s, np.float32)
+        assert fq.shape == (c["L"], 4, self.B, max(c["hid"], c["inter"])), fq.shape
+        assert fs.shape == (c["L"], 4, self.B), fs.shape
+        logits = np.empty((self.B, c["V"]), np.float32)
+        nxt = np.empty(self.B, np.int32)
+        stats = np.zeros((c["L"], 4, 3), np.float32)
+        rc = self.o.lib.oracle_decoder_step_forced(
+            self.h, _ptr(tokens, _i32p), _ptr(pos, _i32p), attn_scale, _ptr(logits, _f32p),
+            _ptr(nxt, _i32p), _ptr(fq, _i8p), _ptr(fs, _f32p), _ptr(stats, _f32p))
+        assert rc == 0, rc
+        return logits, nxt, stats
+
     def step(self, tokens, pos, attn_scale=1.0, layers=-1, lm_head=True):
         c = self.cfg
         tokens = np.ascontiguousarray(tokens, np.int32)
@@ -231,6 +256,17 @@ class OracleDecoder:
 # ---------------------------------------------------------------------------
 # numpy helpers shared by tests / bench (host-side data preparation)
 # ---------------------------------------------------------------------------
+
+def unpack_a_i8(packed: np.ndarray, rows: int, K: int) -> np.ndarray:
+    """[rows][K] int8 from the packed-A order of the GPU's GEMM inputs
+    (csrc/common.hpp a_frag_off_i8: one 1 KiB block per (16-row tile, 64-k
+    step); lane l = row l&15 + 16 * ((k&63) >> 4), 16 consecutive k per lane)."""
+    KS = K // 64
+    m = np.arange(rows)[:, None]
+    k = np.arange(K)[None, :]
+    off = ((((m >> 4) * KS + (k >> 6)) * 64 + (m & 15) + 16 * ((k & 63) >> 4)) * 16 + (k & 15))
+    return np.asarray(packed).reshape(-1)[off]
+
 
 def quantize_rows_np(x: np.ndarray):
     """numpy mirror of int8_quant.cpp per-row quantisation (round half away)."""

@@ -3,7 +3,7 @@
 //
 // Links the reference's own compilable sources, where they lie under
 // /root/reference (see Makefile in this directory):
-//   kv_cache/kv_tile_cache_cpu.cpp   KVTileCacheCPU<float>  (put/get)
+//   kv_cache/kv_tile_cache_cpu.cpp   KVTileCacheCPU<float|uint16_t|int8_t>  (put/get/save/load)
 //   attention_cpu/softmax_lut.cpp    softmax_lut_vec, apply_topk_topp_filter
 //   attention_cpu/int8_quant.cpp     quantize_to_int8, batch_quantize, ...
 //   decoder/layer_norm.hpp, decoder/mlp.hpp, decoder/token_embedding.hpp (header-only)
@@ -199,8 +199,44 @@ static int run_embed(int argc, char** argv) {
   return 0;
 }
 
+// KVTileCacheCPU<T>::save / load (kv_cache/kv_tile_cache_cpu.cpp:89-123): the
+// reference's on-disk tile-record format.  Inputs: idx.i32 [n][3] (batch, head,
+// tile) and data.bin (n tiles of tile_elems elements of T, raw bits).  The
+// reference's save() writes tiles.bin; a second cache load()s it and get()s
+// every index back into back.bin, so the fixture pins both directions.
+template <typename T>
+static int kvtiles_t(const std::string& dir, int n, int tile_elems) {
+  auto idx = read_file<int32_t>(dir + "/idx.i32", (size_t)n * 3);
+  auto data = read_file<T>(dir + "/data.bin", (size_t)n * tile_elems);
+  KVTileCacheCPU<T> c(n + 1, tile_elems);
+  for (int i = 0; i < n; ++i)
+    c.put(idx[3 * i], idx[3 * i + 1], idx[3 * i + 2], data.data() + (size_t)i * tile_elems);
+  c.save(dir + "/tiles.bin");
+  KVTileCacheCPU<T> r(n + 1, tile_elems);
+  r.load(dir + "/tiles.bin");
+  std::vector<T> back((size_t)n * tile_elems);
+  for (int i = 0; i < n; ++i) {
+    const T* t = r.get(idx[3 * i], idx[3 * i + 1], idx[3 * i + 2]);
+    if (!t) { std::fprintf(stderr, "record %d lost in load\n", i); return 3; }
+    std::copy(t, t + tile_elems, back.begin() + (size_t)i * tile_elems);
+  }
+  write_file(dir + "/back.bin", back.data(), back.size());
+  return 0;
+}
+
+// kvtiles <dir> n tile_elems elem_bytes(1|2|4)
+static int run_kvtiles(int argc, char** argv) {
+  if (argc < 6) return 1;
+  const std::string dir = argv[2];
+  const int n = atoi(argv[3]), te = atoi(argv[4]), es = atoi(argv[5]);
+  if (es == 1) return kvtiles_t<int8_t>(dir, n, te);
+  if (es == 2) return kvtiles_t<uint16_t>(dir, n, te);
+  if (es == 4) return kvtiles_t<float>(dir, n, te);
+  return 1;
+}
+
 int main(int argc, char** argv) {
-  if (argc < 2) { std::fprintf(stderr, "usage: gen_golden <attn|softmax|quant|ln|mlp|embed> ...\n"); return 1; }
+  if (argc < 2) { std::fprintf(stderr, "usage: gen_golden <attn|softmax|quant|ln|mlp|embed|kvtiles> ...\n"); return 1; }
   const std::string cmd = argv[1];
   if (cmd == "attn") return run_attn(argc, argv);
   if (cmd == "softmax") return run_softmax(argc, argv);
@@ -208,5 +244,6 @@ int main(int argc, char** argv) {
   if (cmd == "ln") return run_ln(argc, argv);
   if (cmd == "mlp") return run_mlp(argc, argv);
   if (cmd == "embed") return run_embed(argc, argv);
+  if (cmd == "kvtiles") return run_kvtiles(argc, argv);
   return 1;
 }

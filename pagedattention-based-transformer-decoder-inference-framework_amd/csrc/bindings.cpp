@@ -214,6 +214,11 @@ class Decoder {
     py::gil_scoped_release nogil;
     check(llm_decoder_sync(d_));
   }
+  // llm_decoder_set_taps: device pointers (0, 0 switches the taps off)
+  void set_taps(uintptr_t q_ptr, uintptr_t s_ptr) {
+    py::gil_scoped_release nogil;
+    check(llm_decoder_set_taps(d_, reinterpret_cast<int8_t*>(q_ptr), reinterpret_cast<float*>(s_ptr)));
+  }
   int context_len(int row) const { return llm_decoder_context_len(d_, row); }
   uintptr_t kv_handle() const { return reinterpret_cast<uintptr_t>(llm_decoder_kv(d_)); }
   const llm_decoder_config& config() const { return cfg_; }
@@ -284,8 +289,28 @@ class KVTileCache {
   void fork(int src, int dst) { need(); check(kv_cache_fork(c_, src, dst)); }
   void release(int beam) { need(); check(kv_cache_release(c_, beam)); }
   void sync_page_table_to_gpu() { need(); check(kv_cache_sync(c_, nullptr)); check(llm_sync()); }
-  void save_to_file(const std::string& p) { need(); check(kv_cache_save(c_, p.c_str())); }
-  void load_from_file(const std::string& p) { need(); check(kv_cache_load(c_, p.c_str())); }
+  // KVTileCache::save_to_file / load_from_file (kv_tile_cache.cpp:105-125):
+  // format "pools" (default) is the reference's file byte for byte (raw K pool
+  // then V pool; the page table stays as it is); "snapshot" is this build's
+  // file that also restores the layered page table.
+  void save_to_file(const std::string& p, const std::string& format) {
+    need();
+    check(fmt(format) ? kv_cache_save(c_, p.c_str()) : kv_cache_save_pools(c_, p.c_str()));
+  }
+  void load_from_file(const std::string& p, const std::string& format) {
+    need();
+    check(fmt(format) ? kv_cache_load(c_, p.c_str()) : kv_cache_load_pools(c_, p.c_str()));
+  }
+  // KVTileCacheCPU<T>::save / load (kv_tile_cache_cpu.cpp:89-123): the K ("k")
+  // or V ("v") tiles of one layer as the reference's record file
+  void save_tiles(const std::string& p, const std::string& kind, int layer) {
+    need();
+    check(kv_cache_save_tiles(c_, layer, kind_of(kind), p.c_str()));
+  }
+  void load_tiles(const std::string& p, const std::string& kind, int layer) {
+    need();
+    check(kv_cache_load_tiles(c_, layer, kind_of(kind), p.c_str()));
+  }
   // k / v: C-contiguous [n][H][D] arrays whose items are the cache's element
   // bits (fp16/bf16 as uint16 or float16, float32, int8).
   void write_tokens(int layer, int beam, int pos, py::array k, py::array v) {
@@ -318,6 +343,16 @@ class KVTileCache {
 
  private:
   static int llm_sync() { return LLM_OK; }
+  static bool fmt(const std::string& f) {
+    if (f == "pools") return false;
+    if (f == "snapshot") return true;
+    throw std::invalid_argument("KVTileCache: format must be 'pools' (the reference's file) or 'snapshot'");
+  }
+  static int kind_of(const std::string& k) {
+    if (k == "k" || k == "K") return 0;
+    if (k == "v" || k == "V") return 1;
+    throw std::invalid_argument("KVTileCache: kind must be 'k' or 'v'");
+  }
   void need() const { if (!c_) throw std::runtime_error("KVTileCache: call init() first"); }
   kv_cache* c_ = nullptr;
   int tile_size_ = 0, head_dim_ = 0, layers_ = 1, beams_ = 1, heads_ = 1, max_tiles_ = 1;
@@ -383,6 +418,7 @@ PYBIND11_MODULE(llm_decoder, m) {
         .def("step", &Decoder::step, py::arg("tokens") = py::none(), py::arg("logits_ptr") = 0,
              py::arg("stream") = 0, py::arg("want_next") = true)
         .def("sync", &Decoder::sync)
+        .def("set_taps", &Decoder::set_taps, py::arg("q_ptr"), py::arg("s_ptr"))
         .def("context_len", &Decoder::context_len)
         .def_property_readonly("kv_handle", &Decoder::kv_handle);
   };
@@ -417,8 +453,14 @@ PYBIND11_MODULE(llm_decoder, m) {
       .def("fork", &KVTileCache::fork)
       .def("release", &KVTileCache::release)
       .def("sync_page_table_to_gpu", &KVTileCache::sync_page_table_to_gpu)
-      .def("save_to_file", &KVTileCache::save_to_file)
-      .def("load_from_file", &KVTileCache::load_from_file)
+      .def("save_to_file", &KVTileCache::save_to_file, py::arg("path"),
+           py::arg("format") = "pools")
+      .def("load_from_file", &KVTileCache::load_from_file, py::arg("path"),
+           py::arg("format") = "pools")
+      .def("save_tiles", &KVTileCache::save_tiles, py::arg("path"), py::arg("kind") = "k",
+           py::arg("layer") = 0)
+      .def("load_tiles", &KVTileCache::load_tiles, py::arg("path"), py::arg("kind") = "k",
+           py::arg("layer") = 0)
       .def("write_tokens", &KVTileCache::write_tokens)
       .def("view", &KVTileCache::view, py::arg("layer") = 0)
       .def("free_pages", &KVTileCache::free_pages)

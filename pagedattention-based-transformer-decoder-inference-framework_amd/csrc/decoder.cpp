@@ -97,6 +97,12 @@ struct llm_decoder {
   hipGraphExec_t graph = nullptr;
   int graph_batch = -1;
 
+  // activation taps (llm_decoder_set_taps): the int8 GEMM inputs and row scales
+  // of every layer, copied out by the step for teacher-forced parity checks
+  int8_t* tap_q = nullptr;
+  float* tap_s = nullptr;
+  int tap(int l, int stage, const struct Rows& R, int K, hipStream_t st);
+
   ~llm_decoder() {
     if (graph) (void)hipGraphExecDestroy(graph);
     if (kv) kv_cache_destroy(kv);
@@ -394,6 +400,7 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   if (wdtype == LLM_I8) {
     LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
                                        static_cast<int8_t*>(R.act), R.sa, st, 1));
+    RET_IF(tap(l, 0, R, hid, st));
     g.sa = R.sa; g.sw = sw_qkv.p + (size_t)l * 3 * hid;
   } else {
     LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, R.act, st, 1));
@@ -446,14 +453,16 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.A = R.act;
   g.M = R.n;
   // o_proj: input produced (packed) by the attention merge
+  if (i8) RET_IF(tap(l, 1, R, hid, st));
   g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = R.x;
   if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
   RET_IF(weight_gemm(g, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
-  if (i8)
+  if (i8) {
     LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
                                        static_cast<int8_t*>(R.act), R.sa, st, 1));
-  else
+    RET_IF(tap(l, 2, R, hid, st));
+  } else
     LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, R.act, st, 1));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
@@ -470,8 +479,10 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.C16 = nullptr;
   if (!i8) g.A = R.act2;
   // quantise h1 -> mlp_fc2 (+b2)
-  if (i8)
+  if (i8) {
     LLM_HIP_RET(launch_quantize_rows(R.h1, R.n, inter, static_cast<int8_t*>(R.act), R.sa, st, 1));
+    RET_IF(tap(l, 3, R, inter, st));
+  }
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
@@ -496,6 +507,21 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
   R.attn_ws = ws;
   R.attn_ws_bytes = attn_ws_bytes;
   return R;
+}
+
+// Tap stage `stage` of layer l (0: LN1 out, 1: attention out, 2: LN2 out,
+// 3: fc1 out): the rows' packed int8 activations (K per row) and row scales.
+// Decode rows only (prefill chunks are not tapped); captured into the graph.
+int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
+  if (!tap_q || R.prefill_row >= 0 || R.beam_rows) return LLM_OK;
+  const size_t slot = (size_t)l * 4 + stage;
+  const size_t n16 = ((size_t)R.n + 15) / 16 * 16;
+  const size_t r0 = (size_t)R.table_row0;  // rows r0.. of the step (16-row aligned)
+  LLM_HIP_RET(hipMemcpyAsync(tap_q + slot * b16 * qa_ld + r0 * K, R.act, n16 * K,
+                             hipMemcpyDeviceToDevice, st));
+  LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, R.sa, sizeof(float) * R.n,
+                             hipMemcpyDeviceToDevice, st));
+  return LLM_OK;
 }
 
 // LM head + token choice for rows r0.. (x rows given): logits into the step's
@@ -709,6 +735,7 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   LLM_REQUIRE(batch > 0 && batch <= d->maxB, "decoder: batch must be in [1, max_batch]");
   RET_IF(kv_cache_clear(d->kv));
   d->batch = batch;
+  if (d->row_group != 1) d->graph_batch = -1;  // the captured attention launch used the beam group
   d->row_group = 1;
   d->h_pos.assign(d->maxB, 0);
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
@@ -805,6 +832,19 @@ extern "C" int llm_decoder_set_sampling(llm_decoder* d, float temperature, int t
   return LLM_OK;
 }
 
+extern "C" int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev) {
+  LLM_REQUIRE(d, "llm_decoder_set_taps: NULL");
+  LLM_REQUIRE((q_dev == nullptr) == (s_dev == nullptr),
+              "llm_decoder_set_taps: give both tap buffers or neither");
+  LLM_REQUIRE(!q_dev || d->wdtype == LLM_I8, "llm_decoder_set_taps: INT8 decoders only");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_HIP_RET(hipStreamSynchronize(d->stream));
+  d->tap_q = q_dev;
+  d->tap_s = s_dev;
+  d->graph_batch = -1;  // the step graph gains / loses the tap copies
+  return LLM_OK;
+}
+
 extern "C" int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
                                 int32_t* next_host, void* stream) {
   LLM_REQUIRE(d, "llm_decoder_step: NULL");
@@ -829,8 +869,24 @@ extern "C" int llm_decoder_generate(llm_decoder* d, const int32_t* prompts,
                                     int max_gen_len, float temperature, int32_t* out) {
   LLM_REQUIRE(d && prompts && prompt_lens && out, "llm_decoder_generate: NULL");
   LLM_REQUIRE(max_gen_len >= 0, "llm_decoder_generate: max_gen_len < 0");
-  (void)temperature;  // greedy argmax is invariant to temperature > 0 (cuda_decoder.cu:7-14)
+  // generate is greedy argmax whatever the temperature, as the reference's
+  // sample_from_logits (decoder/cuda_decoder.cu:7-14): argmax is invariant to
+  // temperature > 0.  A device-sampling mode set by llm_decoder_set_sampling
+  // applies to llm_decoder_step only; it is suspended here and restored after.
+  (void)temperature;
   std::lock_guard<std::mutex> g(d->mu);
+  struct SamplingGuard {
+    llm_decoder* d;
+    float t;
+    bool active;
+    explicit SamplingGuard(llm_decoder* dd)
+        : d(dd), t(dd->temperature), active(dd->temperature > 0.f && dd->top_k != 1) {
+      if (active) { d->temperature = 0.f; d->graph_batch = -1; }
+    }
+    ~SamplingGuard() {
+      if (active) { d->temperature = t; d->graph_batch = -1; }
+    }
+  } sampling_guard(d);
   LLM_REQUIRE(batch >= 1 && batch <= d->maxB, "llm_decoder_generate: batch out of range");
   int max_len = 0;
   for (int b = 0; b < batch; ++b) {

@@ -18,4 +18,4 @@ int fail(int status, const std::string& msg) {
 
 extern "C" const char* llm_last_error(void) { return llm::g_last_error.c_str(); }
 
-extern "C" int llm_abi_version(void) { return 2; }
+extern "C" int llm_abi_version(void) { return 3; }

@@ -237,10 +237,6 @@ int KvCache::sync(hipStream_t st) {
 
 using namespace llm;
 
-struct kv_cache {
-  KvCache impl;
-};
-
 extern "C" int kv_cache_create(int num_layers, int num_beams, int num_heads, int head_dim,
                                int page_size, int max_tiles, long long num_pages, kv_cache** out) {
   return kv_cache_create_typed(num_layers, num_beams, num_heads, head_dim, page_size, max_tiles,
@@ -470,88 +466,4 @@ extern "C" int32_t* kv_cache_page_table(kv_cache* c, int layer) {
   if (!c || layer < 0 || layer >= c->impl.L) return nullptr;
   const KvCache& k = c->impl;
   return k.d_table + (size_t)layer * k.beams * k.H * k.max_tiles;
-}
-
-namespace {
-constexpr uint64_t kMagic = 0x31564B4D49505041ull;    // "APPIMKV1": fp16 pools, 8-word header
-constexpr uint64_t kMagicV2 = 0x32564B4D49505041ull;  // "APPIMKV2": + kv_dtype word
-}
-
-extern "C" int kv_cache_save(const kv_cache* c, const char* path) {
-  LLM_REQUIRE(c && path, "kv_cache_save: NULL");
-  auto& k = const_cast<kv_cache*>(c)->impl;
-  std::lock_guard<std::mutex> g(k.mu);
-  std::ofstream f(path, std::ios::binary);
-  if (!f) return fail(LLM_ERR_IO, std::string("kv_cache_save: cannot open ") + path);
-  const int64_t hdr[9] = {(int64_t)kMagicV2, k.L, k.beams, k.H, k.D, k.TS, k.max_tiles, k.num_pages,
-                          k.dtype};
-  f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
-  f.write(reinterpret_cast<const char*>(k.h_table.data()), k.entries * sizeof(int32_t));
-  std::vector<int32_t> used;
-  for (long long p = 0; p < k.num_pages; ++p)
-    if (k.refcount[p] > 0) used.push_back((int32_t)p);
-  const int64_t nu = (int64_t)used.size();
-  f.write(reinterpret_cast<const char*>(&nu), sizeof(nu));
-  f.write(reinterpret_cast<const char*>(used.data()), used.size() * sizeof(int32_t));
-  const size_t pb = k.page_bytes();
-  std::vector<char> buf(pb);
-  LLM_HIP_RET(hipDeviceSynchronize());
-  for (int32_t p : used) {
-    // file order per page: K then V (the pool's own page order)
-    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.k_pool + (size_t)p * k.page_stride(), pb,
-                          hipMemcpyDeviceToHost));
-    f.write(buf.data(), pb);
-    LLM_HIP_RET(hipMemcpy(buf.data(), (char*)k.v_pool + (size_t)p * k.page_stride(), pb,
-                          hipMemcpyDeviceToHost));
-    f.write(buf.data(), pb);
-  }
-  if (!f) return fail(LLM_ERR_IO, "kv_cache_save: write failed");
-  return LLM_OK;
-}
-
-extern "C" int kv_cache_load(kv_cache* c, const char* path) {
-  LLM_REQUIRE(c && path, "kv_cache_load: NULL");
-  KvCache& k = c->impl;
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return fail(LLM_ERR_IO, std::string("kv_cache_load: cannot open ") + path);
-  int64_t hdr[9];
-  f.read(reinterpret_cast<char*>(hdr), 8 * sizeof(int64_t));
-  if (!f || (hdr[0] != (int64_t)kMagic && hdr[0] != (int64_t)kMagicV2))
-    return fail(LLM_ERR_IO, "kv_cache_load: bad header");
-  hdr[8] = LLM_F16;
-  if (hdr[0] == (int64_t)kMagicV2) f.read(reinterpret_cast<char*>(&hdr[8]), sizeof(int64_t));
-  if (!f) return fail(LLM_ERR_IO, "kv_cache_load: bad header");
-  if (hdr[1] != k.L || hdr[2] != k.beams || hdr[3] != k.H || hdr[4] != k.D || hdr[5] != k.TS ||
-      hdr[6] != k.max_tiles || hdr[7] != k.num_pages)
-    return fail(LLM_ERR_INVALID, "kv_cache_load: file geometry differs from this cache");
-  if (hdr[8] != k.dtype)
-    return fail(LLM_ERR_INVALID, "kv_cache_load: file kv_dtype differs from this cache");
-  int rc = kv_cache_clear(c);
-  if (rc) return rc;
-  std::lock_guard<std::mutex> g(k.mu);
-  f.read(reinterpret_cast<char*>(k.h_table.data()), k.entries * sizeof(int32_t));
-  int64_t nu = 0;
-  f.read(reinterpret_cast<char*>(&nu), sizeof(nu));
-  if (!f || nu < 0 || nu > k.num_pages) return fail(LLM_ERR_IO, "kv_cache_load: truncated");
-  std::vector<int32_t> used((size_t)nu);
-  f.read(reinterpret_cast<char*>(used.data()), used.size() * sizeof(int32_t));
-  const size_t pb = k.page_bytes();
-  std::vector<char> buf(pb);
-  for (int32_t p : used) {
-    f.read(buf.data(), pb);
-    LLM_HIP_RET(hipMemcpy((char*)k.k_pool + (size_t)p * k.page_stride(), buf.data(), pb,
-                          hipMemcpyHostToDevice));
-    f.read(buf.data(), pb);
-    LLM_HIP_RET(hipMemcpy((char*)k.v_pool + (size_t)p * k.page_stride(), buf.data(), pb,
-                          hipMemcpyHostToDevice));
-  }
-  if (!f) return fail(LLM_ERR_IO, "kv_cache_load: truncated page data");
-  // rebuild refcounts / free list from the table
-  std::fill(k.refcount.begin(), k.refcount.end(), 0);
-  for (size_t i = 0; i < k.entries; ++i)
-    if (k.h_table[i] >= 0 && k.h_table[i] < k.num_pages) k.refcount[k.h_table[i]] += 1;
-  k.reset_free_lists();
-  LLM_HIP_RET(hipMemcpy(k.d_table, k.h_table.data(), k.entries * sizeof(int32_t),
-                        hipMemcpyHostToDevice));
-  return LLM_OK;
 }

@@ -72,5 +72,7 @@ struct KvCache {
 
 }  // namespace llm
 
-struct kv_cache;
+struct kv_cache {
+  llm::KvCache impl;
+};
 llm::KvCache* kv_impl(kv_cache* c);

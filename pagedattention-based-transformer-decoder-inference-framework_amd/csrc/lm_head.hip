@@ -14,8 +14,11 @@
 // (each wave one 16-row tile), all M rows of x.  x is the operand every
 // workgroup shares: it is staged per 256-wide K chunk into LDS once per
 // workgroup (converted to hi/lo A fragments on the way), so the per-CU
-// traffic is E once plus x once per 128 vocabulary rows, instead of x once
+// traffic is E once plus x once per 256 vocabulary rows, instead of x once
 // per 16-32 rows as in a plain tile GEMM (the previous form: 146 us at C3).
+// Registers (scripts/kernel_resources.sh, gfx950): lm_head_kernel<1|2|4>
+// (M tiles of 16 rows) use 100 / 104 / 124 VGPRs with no scratch, inside the
+// 128 that __launch_bounds__(1024) leaves.
 // E fragments for the next chunk are in flight while the current one is
 // multiplied.
 //

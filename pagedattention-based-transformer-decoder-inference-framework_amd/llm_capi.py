@@ -104,6 +104,12 @@ _SIGS = {
     "kv_cache_page_table": (c_void_p, [c_void_p, c_int]),
     "kv_cache_save": (c_int, [c_void_p, ctypes.c_char_p]),
     "kv_cache_load": (c_int, [c_void_p, ctypes.c_char_p]),
+    "kv_cache_inspect": (c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]),
+    "kv_cache_save_pools": (c_int, [c_void_p, ctypes.c_char_p]),
+    "kv_cache_load_pools": (c_int, [c_void_p, ctypes.c_char_p]),
+    "kv_cache_save_tiles": (c_int, [c_void_p, c_int, c_int, ctypes.c_char_p]),
+    "kv_cache_load_tiles": (c_int, [c_void_p, c_int, c_int, ctypes.c_char_p]),
+    "kv_tiles_inspect": (c_int, [ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(c_int)]),
 }
 
 _lib = None

@@ -7,7 +7,7 @@
 import sys, re
 cur = None
 for line in sys.stdin:
-    m = re.search(r"remark: (Function Name|VGPRs|AGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\S+)", line)
+    m = re.search(r"remark:\s+(Function Name|ScratchSize \[bytes/lane\]|VGPRs|AGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]|LDS Size \[bytes/block\]): (\S+)", line)
     if not m: continue
     k, v = m.groups()
     if k == "Function Name":

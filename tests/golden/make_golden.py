@@ -5,7 +5,8 @@ reference's own compilable sources (oracle/ref_golden/Makefile) and runs it on
 seeded inputs.  Each fixture holds the inputs AND the reference outputs; the
 reference source itself never enters the repository.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            # every fixture
+    python tests/golden/make_golden.py kvtiles    # only the KV record files
 """
 from __future__ import annotations
 
@@ -140,10 +141,46 @@ def embed_case(name, vocab, hid, n, seed):
     np.savez_compressed(GOLDEN / f"embed_{name}.npz", emb=emb, ids=ids, out=out)
 
 
+def kvtiles_case(name, *, ts, D, dtype, idx, seed):
+    """KVTileCacheCPU<T>::save / load (kv_cache/kv_tile_cache_cpu.cpp:89-123): the
+    reference writes the record file for these tiles, then reads it back."""
+    rng = np.random.default_rng(seed)
+    idx = np.asarray(idx, np.int32).reshape(-1, 3)
+    n, te = len(idx), ts * D
+    if dtype == np.int8:
+        data = rng.integers(-128, 128, (n, ts, D)).astype(np.int8)
+    else:
+        data = rng.standard_normal((n, ts, D)).astype(dtype)
+    es = data.dtype.itemsize
+    with tempfile.TemporaryDirectory() as d:
+        d = Path(d)
+        idx.tofile(d / "idx.i32")
+        data.tofile(d / "data.bin")
+        run("kvtiles", d, n, te, es)
+        file_bytes = np.fromfile(d / "tiles.bin", np.uint8)
+        back = np.fromfile(d / "back.bin", data.dtype).reshape(n, ts, D)
+    np.savez_compressed(GOLDEN / f"kvtiles_{name}.npz", idx=idx, data=data, ts=np.int32(ts),
+                        D=np.int32(D), file_bytes=file_bytes, back=back)
+
+
+def kvtiles_cases():
+    # fp16 pools are KVTileCacheCPU<uint16_t> (kv_tile_cache_cpu.cpp:138); a
+    # beam/head/tile spread with gaps, a repeated beam and tile 0.
+    kvtiles_case("f16_ts16_d64", ts=16, D=64, dtype=np.float16, seed=70,
+                 idx=[(0, 0, 0), (0, 0, 1), (0, 1, 0), (1, 0, 3), (2, 1, 2), (1, 1, 0)])
+    kvtiles_case("f32_ts16_d32", ts=16, D=32, dtype=np.float32, seed=71,
+                 idx=[(0, 1, 1), (1, 0, 0), (0, 0, 2), (1, 1, 1)])
+    kvtiles_case("i8_ts32_d64", ts=32, D=64, dtype=np.int8, seed=72,
+                 idx=[(0, 0, 0), (1, 1, 1), (0, 1, 0)])
+
+
 def main():
     if not Path("/root/reference").exists():
         sys.exit("make_golden.py needs /root/reference (build container only)")
     build_generator()
+    if sys.argv[1:] == ["kvtiles"]:  # only the KV record-file fixtures
+        kvtiles_cases()
+        return
     # C1 attention shapes (B1/H4/D64/T128/ts16) and the edge cases the
     # reference's code paths have: missing tiles, beam routing, temperature,
     # top-k / top-p / EOS filters, ragged last tile, other tile sizes, D=128.
@@ -165,6 +202,7 @@ def main():
     ln_case("r3c256", 3, 256, 40)
     mlp_case("r2h64", 2, 64, 256, 50)
     embed_case("v50", 50, 16, 7, 60)
+    kvtiles_cases()
     print("golden fixtures written to", GOLDEN)
 
 

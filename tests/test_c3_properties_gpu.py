@@ -1,6 +1,7 @@
 """Size-independent properties of the decoder at the FULL BASELINE C3 size
 (INT8Decoder, 24 layers / 16 heads / head_dim 128, 64 rows, KV context 8192
-in shuffled 16-token pages: 103 GB of KV on the card), where the oracle cannot
+in shuffled 16-token pages: 103 GB of KV on the card) and at the C5 per-GPU
+shard (32 layers / 32 heads, 275 GB of KV), where the oracle cannot
 follow every row.  The oracle parity of each piece is in the other GPU tests
 (attention at C3 size in test_pa_decode_gpu.py); these check what only the
 full-size step can show:
@@ -19,11 +20,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_c3_full_size_determinism_and_row_independence(gpu):
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_full_size_determinism_and_row_independence(gpu, name):
+    """c3: the BASELINE metric config; c5: its per-GPU shard (32 layers / 32
+    heads, 64 rows: 275 GB of KV, the page pool fills the card)."""
     import torch
     import llm_decoder
     from bench import CONFIGS, make_weights
-    cfg = CONFIGS["c3"]
+    cfg = CONFIGS[name]
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()  # the c5 pool needs nearly the whole card
     L, H, D, V, B, T, ts = (cfg[k] for k in ("L", "H", "D", "V", "B", "T", "ts"))
     dec = llm_decoder.INT8Decoder(L, H, D, H * D, V, T + 8, max_batch=B, page_size=ts)
     dec.set_weights(make_weights(cfg, 1234))

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_pure_host_helpers():
     import llm_capi
     lib = llm_capi.load()
-    assert lib.llm_abi_version() == 2
+    assert lib.llm_abi_version() == 3
     # host-only sizing helpers (no device calls)
     assert lib.gemm_packed_bytes(llm_capi.LLM_I8, 2048, 6144) == 6144 // 16 * 2048 // 64 * 1024
     assert lib.gemm_packed_bytes(llm_capi.LLM_F16, 768, 2304) == 2304 // 16 * 768 // 32 * 1024

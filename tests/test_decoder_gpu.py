@@ -3,26 +3,35 @@
 
 Every kernel of the step is held to its own bar elsewhere (int32 GEMM
 accumulators and epilogues bit-exact, row quantiser bit-exact, attention 1e-7
-rel).  A whole step is NOT bit-exact and cannot be: LayerNorm / softmax reduce
-in a different fp32 order (~1e-7 rel), and once in a while that moves an
-activation across an int8 rounding boundary.  One flipped int8 LSB is 1/127 of
-the row's absmax and changes the layer output by ~0.5% (measured with
-scripts/debug_layer.py: after LN2, 1 of 768 int8 values flipped, every other
-stage bit-exact, layer output off by 6e-3).  Hence:
-  * tokens: every GPU token equals the oracle's argmax unless the oracle's top-2
-    logits are within TIE_TOL of the logit scale (both sides are then fed the
-    GPU's token, so a tie cannot cascade);
-  * logits: within LOGIT_TOL rel (max-abs error / max-abs logit) over the run;
-  * the int8 flips themselves must stay rare (checked in
-    test_int8_flip_rate below)."""
+rel).  A whole step is not bit-exact: LayerNorm / softmax reduce in a different
+fp32 order (~1e-7 rel), and once in a while that moves an activation across an
+int8 rounding boundary (one LSB = 1/127 of the row's absmax, ~0.5 % of a layer
+output; scripts/debug_layer.py).
+
+The parity tests therefore run TEACHER-FORCED at the int8 activations
+(llm_decoder_set_taps + OracleDecoder.step_forced): after every GPU step the
+four int8 GEMM inputs of every layer are read back; the oracle quantises its own
+fp32 values, counts where they differ from the GPU's (one LSB at most, rare),
+and continues from the GPU's.  A flip can then not propagate, and the step is
+held to the north_star bar:
+  * logits within LOGIT_TOL = 1e-3 rel (max-abs error / max-abs logit) at every
+    step — measured ~1e-6;
+  * tokens exact: a GPU token may differ from the oracle's argmax only where the
+    oracle's top two logits are within TIE_TOL = 1e-5 of the logit scale (a tie
+    at fp32 noise level);
+  * int8 activations: every GPU value within one LSB of the oracle's, flips
+    below 1e-3 of all values.
+The free-running tests (no forcing: prompts, generate, prefill) let flips
+propagate and are held to FREE_RUN_TOL, a drift bound, not a parity bar."""
 import numpy as np
 import pytest
 
 from _util import rel_err
 
 pytestmark = pytest.mark.gpu
-TIE_TOL = 5e-2
-LOGIT_TOL = 5e-2
+LOGIT_TOL = 1e-3
+TIE_TOL = 1e-5
+FREE_RUN_TOL = 5e-2
 
 
 def _torch():
@@ -50,8 +59,8 @@ def _make_gpu_decoder(w, max_batch, cls="INT8Decoder"):
     return dec
 
 
-def _teacher_forced(dec, odec, steps, B, V, seed):
-    """Random tokens every step (no feedback): strict logits parity."""
+def _random_tokens(dec, odec, steps, B, V, seed):
+    """Random tokens every step (no feedback), free running: drift bound."""
     torch = _torch()
     dec.begin_synthetic(B, 0, 0, False)
     logits = torch.empty((B, V), device="cuda")
@@ -67,7 +76,7 @@ def _teacher_forced(dec, odec, steps, B, V, seed):
         for b in range(B):
             if g_next[b] != o_next[b]:
                 gap = o_logits[b][o_next[b]] - o_logits[b][g_next[b]]
-                assert gap <= TIE_TOL * np.abs(o_logits[b]).max()
+                assert gap <= FREE_RUN_TOL * np.abs(o_logits[b]).max()
     return worst
 
 
@@ -94,7 +103,7 @@ def _lockstep(dec, odec, prompts, gen, V):
                 top = np.sort(o_logits[b])[-2:]
                 scale = np.abs(o_logits[b]).max()
                 gap = o_logits[b][o_next[b]] - o_logits[b][g_next[b]]
-                assert gap <= TIE_TOL * scale, (s, b, g_next[b], o_next[b], gap, top)
+                assert gap <= FREE_RUN_TOL * scale, (s, b, g_next[b], o_next[b], gap, top)
                 ties += 1
             if s >= len(prompts[b]) - 1 and len(out[b]) < gen:
                 out[b].append(g_next[b])
@@ -102,35 +111,128 @@ def _lockstep(dec, odec, prompts, gen, V):
     return out, ties, worst
 
 
+class _Taps:
+    """Device buffers of llm_decoder_set_taps and their host unpacking into the
+    oracle's forced-activation layout [L][4][B][max(hid, inter)]."""
+
+    def __init__(self, dec, w, max_batch):
+        torch = _torch()
+        c = w["cfg"]
+        self.L, self.hid, self.inter = c["L"], c["hid"], c["inter"]
+        self.K = max(self.hid, self.inter)
+        self.b16 = (max_batch + 15) // 16 * 16
+        self.maxB = max_batch
+        self.q = torch.zeros(self.L * 4 * self.b16 * self.K, dtype=torch.int8, device="cuda")
+        self.s = torch.zeros(self.L * 4 * max_batch, dtype=torch.float32, device="cuda")
+        dec.set_taps(self.q.data_ptr(), self.s.data_ptr())
+
+    def read(self, B):
+        from oracle.oracle import unpack_a_i8
+        q = self.q.cpu().numpy().reshape(self.L, 4, self.b16 * self.K)
+        s = self.s.cpu().numpy().reshape(self.L, 4, self.maxB)
+        fq = np.zeros((self.L, 4, B, self.K), np.int8)
+        for l in range(self.L):
+            for st in range(4):
+                Kst = self.inter if st == 3 else self.hid
+                fq[l, st, :, :Kst] = unpack_a_i8(q[l, st, :self.b16 * Kst], B, Kst)
+        return fq, np.ascontiguousarray(s[:, :, :B])
+
+
+def _forced_lockstep(dec, odec, taps, prompts, gen, V):
+    """Step the GPU (taps on) and the teacher-forced oracle together; prompts
+    are fed one token per step, then each row's own (GPU) next token.  Holds
+    every step to LOGIT_TOL / TIE_TOL; returns (tokens per row, worst logit
+    error, int8 values compared, int8 values that differed)."""
+    torch = _torch()
+    B = len(prompts)
+    steps = max(len(p) for p in prompts) + gen - 1
+    dec.begin_synthetic(B, 0, 0, False)
+    logits = torch.empty((B, V), device="cuda")
+    out = [[] for _ in range(B)]
+    nxt = [0] * B
+    worst, n_vals, n_flips = 0.0, 0, 0
+    for s in range(steps):
+        tok = [p[s] if s < len(p) else nxt[b] for b, p in enumerate(prompts)]
+        g_next = dec.step(tok, logits_ptr=logits.data_ptr())
+        torch.cuda.synchronize()
+        fq, fs = taps.read(B)
+        o_logits, o_next, stats = odec.step_forced(np.array(tok, np.int32),
+                                                   np.full(B, s, np.int32), fq, fs)
+        gl = logits.cpu().numpy()
+        err = rel_err(gl, o_logits)
+        assert err < LOGIT_TOL, (s, err)
+        worst = max(worst, err)
+        assert stats[:, :, 1].max() <= 1, (s, stats)        # at most one int8 LSB
+        assert stats[:, :, 2].max() < 1e-5, (s, stats)      # row scales agree
+        n_flips += int(stats[:, :, 0].sum())
+        n_vals += B * taps.L * (3 * taps.hid + taps.inter)
+        for b in range(B):
+            if g_next[b] != o_next[b]:
+                gap = o_logits[b][o_next[b]] - o_logits[b][g_next[b]]
+                assert gap <= TIE_TOL * np.abs(o_logits[b]).max(), (s, b, gap)
+            if s >= len(prompts[b]) - 1 and len(out[b]) < gen:
+                out[b].append(g_next[b])
+        nxt = list(g_next)
+    return out, worst, n_vals, n_flips
+
+
 def test_int8_decoder_matches_oracle_c1(gpu, oracle):
-    """C1 model dims (2 layers, 4 heads, d=64, tile 16), ragged prompts."""
+    """C1 model dims (2 layers, 4 heads, d=64, tile 16), ragged prompts, 46
+    teacher-forced steps at the north_star bar (logits 1e-3, exact tokens)."""
     from oracle.oracle import OracleDecoder
     w = _int8_model(oracle, L=2, H=4, D=64, V=1000, S=64)
     dec = _make_gpu_decoder(w, max_batch=3)
-    odec = OracleDecoder(oracle, w, 3)
+    taps = _Taps(dec, w, 3)
     rng = np.random.default_rng(0)
     prompts = [list(rng.integers(0, 1000, n)) for n in (5, 17, 1)]
-    out, ties, worst = _lockstep(dec, odec, prompts, gen=20, V=1000)
-    assert worst < LOGIT_TOL, worst
-    assert ties <= 0.05 * 3 * 36  # disagreements (all near ties) among token decisions
-    assert all(len(o) == 20 for o in out)
-    odec2 = OracleDecoder(oracle, w, 3)
-    assert _teacher_forced(dec, odec2, 40, 3, 1000, seed=1) < LOGIT_TOL
+    out, worst, n_vals, n_flips = _forced_lockstep(dec, OracleDecoder(oracle, w, 3), taps,
+                                                   prompts, gen=30, V=1000)
+    assert all(len(o) == 30 for o in out)
+    assert n_flips < 1e-3 * n_vals, (n_flips, n_vals)
+    print(f"C1 forced lockstep: worst logit rel err {worst:.2e}, int8 flips {n_flips}/{n_vals}")
+    # free running (no taps): the same decoder, flips allowed to propagate
+    dec.set_taps(0, 0)
+    assert _random_tokens(dec, OracleDecoder(oracle, w, 3), 40, 3, 1000, seed=1) < FREE_RUN_TOL
 
 
 def test_int8_decoder_larger_heads(gpu, oracle):
-    """D=128 heads, several pages per row, a row crossing page boundaries."""
+    """D=128 heads, several pages per row, a row crossing page boundaries;
+    teacher forced over 69 steps."""
     from oracle.oracle import OracleDecoder
     w = _int8_model(oracle, L=2, H=2, D=128, V=512, S=96, seed=7)
     dec = _make_gpu_decoder(w, max_batch=2)
-    odec = OracleDecoder(oracle, w, 2)
+    taps = _Taps(dec, w, 2)
     rng = np.random.default_rng(1)
     prompts = [list(rng.integers(0, 512, 40)), list(rng.integers(0, 512, 3))]
-    _, ties, worst = _lockstep(dec, odec, prompts, gen=30, V=512)
-    assert worst < LOGIT_TOL, worst
-    assert ties <= 0.05 * 2 * 69
-    odec2 = OracleDecoder(oracle, w, 2)
-    assert _teacher_forced(dec, odec2, 70, 2, 512, seed=2) < LOGIT_TOL
+    _, worst, n_vals, n_flips = _forced_lockstep(dec, OracleDecoder(oracle, w, 2), taps,
+                                                 prompts, gen=30, V=512)
+    assert n_flips < 1e-3 * n_vals, (n_flips, n_vals)
+    dec.set_taps(0, 0)
+    _, _, worst_free = _lockstep(dec, OracleDecoder(oracle, w, 2), prompts, gen=30, V=512)
+    assert worst_free < FREE_RUN_TOL, worst_free
+
+
+def test_generate_after_set_sampling_is_greedy(gpu, oracle):
+    """generate is greedy argmax (sample_from_logits, decoder/cuda_decoder.cu:
+    7-14) even after set_sampling; the sampling mode still applies to step."""
+    w = _int8_model(oracle, L=1, H=2, D=64, V=300, S=48, seed=3)
+    dec = _make_gpu_decoder(w, max_batch=2)
+    prompt = [3, 14, 15, 92]
+    greedy = dec.generate(prompt, 10, 1.0)
+    dec.set_sampling(1.5, 0, 1.0, 123)
+    assert dec.generate(prompt, 10, 1.0) == greedy
+    assert dec.generate(prompt, 10, 0.5) == greedy
+    # step still samples: at temperature 1.5 over 300 tokens, 16 draws are
+    # not all the argmax of their own step's logits
+    torch = _torch()
+    logits = torch.empty((2, 300), device="cuda")
+    dec.begin_synthetic(2, 0, 0, False)
+    tok, differ = [5, 6], 0
+    for _ in range(8):
+        tok = dec.step(tok, logits_ptr=logits.data_ptr(), want_next=True)
+        torch.cuda.synchronize()
+        differ += int((np.asarray(tok) != logits.cpu().numpy().argmax(1)).sum())
+    assert differ > 0
 
 
 def test_generate_call_forms(gpu, oracle):
@@ -404,7 +506,7 @@ def test_prefill_matches_token_by_token(gpu, oracle, monkeypatch, mfma):
     one row per token — only the split order differs: 1e-4 rel.
     mfma=1 (default): the MFMA prefill kernel, whose attention agrees with the
     decode kernel to ~1e-6 (tests/test_pa_prefill_gpu.py); through the int8
-    activations that is the oracle bar of this file (LOGIT_TOL, near ties)."""
+    activations that is the free-running bar of this file (FREE_RUN_TOL)."""
     monkeypatch.setenv("LLM_PREFILL_MFMA", str(mfma))
     w = _int8_model(oracle, L=2, H=4, D=64, V=500, S=1024, seed=12)
     V = w["cfg"]["V"]
@@ -417,9 +519,9 @@ def test_prefill_matches_token_by_token(gpu, oracle, monkeypatch, mfma):
             assert err < 1e-4, (r, err)
             assert nxt[r] == int(np.argmax(la[r]))
         else:
-            assert err < LOGIT_TOL, (r, err)
+            assert err < FREE_RUN_TOL, (r, err)
             gap = la[r].max() - la[r][nxt[r]]
-            assert gap <= TIE_TOL * np.abs(la[r]).max()
+            assert gap <= FREE_RUN_TOL * np.abs(la[r]).max()
 
 
 def test_prefill_mfma_fp16_decoder(gpu, oracle, monkeypatch):
@@ -454,12 +556,15 @@ def test_micro_batch_step_vs_oracle(gpu, oracle, monkeypatch, mb, pp):
     """The step graph with the rows split into two micro-batches on two streams
     (LLM_MICROBATCHES=2; 48 rows -> 32 + 16, 16-row packed-A boundary), free
     running or with ping-pong attention ordering, against the oracle —
-    teacher forced, strict logits parity."""
+    teacher forced at the int8 activations, north_star bar."""
     from oracle.oracle import OracleDecoder
-    torch = _torch()
     monkeypatch.setenv("LLM_MICROBATCHES", str(mb))
     monkeypatch.setenv("LLM_MB_PINGPONG", str(pp))
     w = _int8_model(oracle, L=2, H=4, D=64, V=600, S=32, seed=31)
     dec = _make_gpu_decoder(w, max_batch=48)
-    odec = OracleDecoder(oracle, w, 48)
-    assert _teacher_forced(dec, odec, 5, 48, 600, seed=2) < LOGIT_TOL
+    taps = _Taps(dec, w, 48)
+    rng = np.random.default_rng(2)
+    prompts = [list(rng.integers(0, 600, 5)) for _ in range(48)]
+    _, _, n_vals, n_flips = _forced_lockstep(dec, OracleDecoder(oracle, w, 48), taps, prompts,
+                                             gen=3, V=600)
+    assert n_flips < 1e-3 * n_vals

@@ -109,7 +109,8 @@ def test_f16_gemm(gpu, M, K, N):
         assert rel_err(C, ref) < 1e-3
 
 
-@pytest.mark.parametrize("M,V,K", [(64, 50257, 2048), (1, 1000, 256), (16, 50257, 768), (70, 333, 64)])
+@pytest.mark.parametrize("M,V,K", [(64, 50257, 2048), (1, 1000, 256), (16, 50257, 768), (70, 333, 64),
+                                   (17, 4099, 512), (32, 50257, 2048), (24, 257, 128)])
 def test_lm_head(gpu, M, V, K):
     import llm_capi
     rng = np.random.default_rng(V + K)

@@ -137,11 +137,11 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
             assert rel_err(outg, out) < 1e-5
     # save / load round trip
     path = str(tmp_path / "kv.bin")
-    kv.save_to_file(path)
+    kv.save_to_file(path, format="snapshot")
     kv2 = llm_decoder.KVTileCache()
     kv2.init(num_pages=64, tile_size=TS, head_dim=D, num_layers=1, num_beams=beams,
              num_heads=H, max_tiles=8)
-    kv2.load_from_file(path)
+    kv2.load_from_file(path, format="snapshot")
     for b in range(beams):
         for t in range(4):
             assert kv2.lookup(b, 0, t) == kv.lookup(b, 0, t)
@@ -313,11 +313,11 @@ def test_typed_kv_cache_attention_and_save_load(gpu, oracle, tmp_path, dtype):
     ref = oracle.paged_attention(q, kpool, vpool, pt, T=T)
     assert rel_err(out.cpu().numpy(), ref) < 1e-3
     path = str(tmp_path / "kv.bin")
-    kv.save_to_file(path)
+    kv.save_to_file(path, format="snapshot")
     kv2 = llm_decoder.KVTileCache()
     kv2.init(num_pages=32, tile_size=TS, head_dim=D, num_layers=1, num_beams=B, num_heads=H,
              max_tiles=8, dtype=dtype)
-    kv2.load_from_file(path)
+    kv2.load_from_file(path, format="snapshot")
     kv2.sync_page_table_to_gpu()
     out2 = torch.empty_like(out)
     llm_decoder.paged_attention(kv2.handle, 0, qd.data_ptr(), out2.data_ptr(), B=B, H=H, D=D,
@@ -328,4 +328,4 @@ def test_typed_kv_cache_attention_and_save_load(gpu, oracle, tmp_path, dtype):
     other.init(num_pages=32, tile_size=TS, head_dim=D, num_layers=1, num_beams=B, num_heads=H,
                max_tiles=8, dtype="float16")
     with pytest.raises(RuntimeError, match="kv_dtype"):
-        other.load_from_file(path)
+        other.load_from_file(path, format="snapshot")
