@@ -59,6 +59,11 @@ CONFIGS = {
     "c5": dict(cls="INT8Decoder", L=32, H=32, D=128, V=50257, B=64, T=8192, ts=16,
                workload="C5 (per GPU): INT8 decoder, 32-layer/32-head/d=128, 64 seqs/GPU "
                         "(512 over 8 GPUs), KV context 8192, page 16"),
+    # BASELINE.json configs[0]: the reference's CPU-runnable case (INT8Decoder,
+    # batch 1); its CPU baseline is timed end to end (whole steps)
+    "c1": dict(cls="INT8Decoder", L=2, H=4, D=64, V=50257, B=1, T=128, ts=16, cpu_full=True,
+               workload="C1: INT8 decoder, 2-layer/4-head/d=64, batch 1, KV context 128, "
+                        "page 16"),
     # BASELINE.json configs[1]
     "c2": dict(cls="CUDADecoder", L=12, H=12, D=64, V=50257, B=16, T=2048, ts=16,
                workload="C2: fp16 paged decode, 12-layer/12-head/d=64, 16 seqs/GPU, "
@@ -157,47 +162,59 @@ def time_attention(dec, cfg, B, T, max_seq, iters=20, row_group=1):
 
 
 def cpu_baseline(cfg, budget_s=20.0):
-    """Oracle (restated INT8Decoder, C++/OpenMP) on this host: a bounded sample
-    of the same workload — SAMPLE_ROWS of the 64 rows through ONE layer at the
-    full KV context, plus the LM head for those rows; per-token time scaled to
-    all layers."""
-    from oracle.oracle import Oracle, OracleDecoder
-    o = Oracle(bench=True)
-    L, H, D, V, T = cfg["L"], cfg["H"], cfg["D"], cfg["V"], cfg["T"]
+    """The oracle (restated INT8Decoder / CUDADecoder, C++/OpenMP, built with
+    -march=native on this host) timed on this host's cores over a bounded
+    sample of the same workload.  C1 (the reference's own CPU-runnable
+    config) is timed end to end: whole decode steps, every layer and the LM
+    head.  Larger configs: up to 16 of the rows through ONE layer at the full
+    KV context (median of up to 5), scaled to all layers, plus the LM head."""
+    from oracle.oracle import Oracle, OracleDecoder, host_cpu, native_build
+    native = native_build()
+    o = Oracle(bench="native" if native else True)
+    L, H, D, V, T, B = cfg["L"], cfg["H"], cfg["D"], cfg["V"], cfg["T"], cfg["B"]
     hid = H * D
-    rows = 16
-    one = dict(cfg, L=1)
-    w = make_weights(one, 99)
+    full = cfg.get("cpu_full", False)
+    rows = B if full else min(B, 16)
+    layers = L if full else 1
+    mcfg = dict(cfg, L=layers)
+    w = make_weights(mcfg, 99)
     wd = {k: np.ascontiguousarray(v) for k, v in w.items()}
     wd["emb"] = w["emb"].view(np.float16)
-    if cfg["cls"] != "INT8Decoder":
-        return None
-    wd["cfg"] = dict(L=1, H=H, D=D, hid=hid, inter=4 * hid, V=V, max_seq=T + 1)
+    wd["cfg"] = dict(L=layers, H=H, D=D, hid=hid, inter=4 * hid, V=V, max_seq=T + 1)
     dec = OracleDecoder(o, wd, rows)
     rng = np.random.default_rng(0)
-    for which in (0, 1):  # fill the context: positive fp16 values in [0.125, 1)
-        kv = dec.kv(0, which)
-        kv[:, :, :T].view(np.uint16)[...] = rng.integers(0x3000, 0x3C00, kv[:, :, :T].shape,
-                                                          dtype=np.uint16)
+    for l in range(layers):
+        for which in (0, 1):  # fill the context: positive fp16 values in [0.125, 1)
+            kv = dec.kv(l, which)
+            kv[:, :, :T].view(np.uint16)[...] = rng.integers(0x3000, 0x3C00, kv[:, :, :T].shape,
+                                                              dtype=np.uint16)
     toks = np.arange(rows, dtype=np.int32)
     pos = np.full(rows, T, np.int32)
     t0 = time.perf_counter()
-    n_layer = 0
-    t_layer = []
+    times = []
     while True:
         a = time.perf_counter()
-        dec.step(toks, pos, layers=1, lm_head=False)
-        t_layer.append(time.perf_counter() - a)
-        n_layer += 1
-        if time.perf_counter() - t0 > budget_s * 0.6 or n_layer >= 5:
+        dec.step(toks, pos, layers=-1 if full else 1, lm_head=full)
+        times.append(time.perf_counter() - a)
+        if time.perf_counter() - t0 > budget_s * 0.6 or len(times) >= (20 if full else 5):
             break
-    a = time.perf_counter()
-    dec.step(toks, pos, layers=0, lm_head=True)
-    t_lm = time.perf_counter() - a
-    t_step = L * float(np.median(t_layer)) + t_lm
+    if full:
+        t_step = float(np.median(times))
+        sample = (f"{rows} row(s), whole decode steps ({L} layers + LM head) at KV context {T} "
+                  f"(median of {len(times)})")
+    else:
+        a = time.perf_counter()
+        dec.step(toks, pos, layers=0, lm_head=True)
+        t_lm = time.perf_counter() - a
+        t_step = L * float(np.median(times)) + t_lm
+        sample = (f"{rows} of {B} rows, 1 of {L} layers at KV context {T} (median of "
+                  f"{len(times)}) x {L} layers + LM head")
+    lib = "oracle/liboracle_native.so (-O3 -march=native, built on this host)" if native else \
+        "oracle/liboracle_bench.so (-O3 -march=x86-64-v3: the native build failed)"
     return {"value": rows / t_step, "unit": "tokens/s", "cores": o.num_threads(), "kind": "port",
-            "sample": f"{rows} of {cfg['B']} rows, 1 of {L} layers at KV context {T} "
-                      f"(median of {n_layer}) x {L} layers + LM head, oracle/liboracle_bench.so"}
+            "sample": f"{sample}, {lib}",
+            "decoder": "restated " + ("INT8Decoder" if cfg["cls"] == "INT8Decoder" else "CUDADecoder"),
+            "cpu": host_cpu()}
 
 
 def load_traffic(cfg_name):
@@ -225,6 +242,8 @@ def main():
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: this many rows in total, sharded over the ranks "
                          "(default: the config's batch on every rank, weak scaling)")
+    ap.add_argument("--gather", default="logits", choices=["logits", "ids"],
+                    help="N > 1: what each step gathers to rank 0 (SURVEY §8e)")
     ap.add_argument("--seed", type=int, default=1234)
     args = ap.parse_args()
 
@@ -245,14 +264,17 @@ def main():
         else:
             dist.init_process_group(backend)
     import llm_decoder  # noqa: F401  (fails loudly if the HIP build is missing)
+    import dist_decode
 
     cfg = CONFIGS[args.config]
     B, T = cfg["B"], cfg["T"]
     strong = args.global_batch > 0 and "beams" not in cfg
-    if strong:  # rows of this rank
-        if args.global_batch % world:  # the logits gather takes equal shards
-            raise SystemExit(f"--global-batch {args.global_batch} must be a multiple of {world}")
-        B = args.global_batch // world
+    shard_rows = None
+    if strong:  # rows of this rank (ragged shards gather point to point)
+        if args.global_batch < world:
+            raise SystemExit(f"--global-batch {args.global_batch} needs >= {world} rows")
+        shard_rows = dist_decode.shard_sizes(args.global_batch, world)
+        B = shard_rows[rank]
     hid = cfg["H"] * cfg["D"]
     max_seq = T + args.warmup + args.steps + 8
     cls = getattr(llm_decoder, cfg["cls"])
@@ -269,53 +291,17 @@ def main():
         dec.begin_synthetic(B, T, args.seed + rank, True)
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s")
 
-    stream = torch.cuda.current_stream()
-    sp = stream.cuda_stream
-    logits = [torch.empty((B, cfg["V"]), device="cuda") for _ in range(2)]
+    # the multi-rank decode loop (dist_decode.ShardedDecode / timed_run): each
+    # step's logits (or greedy ids, --gather ids) go to rank 0, double-buffered
+    # behind the next step; gloo rehearsals stage them through host memory
     host_gather = world > 1 and backend != "nccl"
-    gather_bufs = ([[torch.empty_like(logits[0], device="cpu" if host_gather else "cuda")
-                     for _ in range(world)] for _ in range(2)]
-                   if world > 1 and rank == 0 else [None, None])
-    works = [None, None]
+    sd = dist_decode.ShardedDecode(
+        dist_decode.HipDecoderStep(dec), B, cfg["V"], world=world, rank=rank,
+        shard_rows=shard_rows, gather=args.gather if world > 1 else "none",
+        staging="host" if host_gather else "device")
     tokens = np.random.default_rng(args.seed + rank).integers(0, cfg["V"], B).astype(np.int32)
-
-    def one_step(i, first):
-        slot = i % 2
-        if works[slot] is not None:
-            works[slot].wait()
-        dec.step(list(map(int, tokens)) if first else None,
-                 logits_ptr=logits[slot].data_ptr() if world > 1 else 0,
-                 stream=sp, want_next=False)
-        if host_gather:
-            dist.gather(logits[slot].cpu(), gather_bufs[slot] if rank == 0 else None, dst=0)
-        elif world > 1:
-            works[slot] = dist.gather(logits[slot], gather_bufs[slot] if rank == 0 else None,
-                                      dst=0, async_op=True)
-
-    for i in range(args.warmup):
-        one_step(i, i == 0)
-    torch.cuda.synchronize()
-    if world > 1:
-        for wk in works:
-            if wk is not None:
-                wk.wait()
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        one_step(i, args.warmup == 0 and i == 0)
-    for wk in works:
-        if wk is not None:
-            wk.wait()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], device="cpu" if host_gather else "cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = dist_decode.timed_run(sd, args.warmup, args.steps, list(map(int, tokens)),
+                                    timer_device="cpu" if host_gather else "cuda")
     t_step = elapsed / args.steps
     T_mean = T + args.warmup + args.steps / 2.0
     value = (args.global_batch if strong else B * world) / t_step
@@ -332,6 +318,10 @@ def main():
             # applied to this launch's algorithmic bytes)
             "traffic": int(ratio * attn_b) if ratio else None,
             "traffic_over_algorithmic": ratio,
+            "traffic_source": (f"profiles/pmc_attention_{args.config}.json: rocprofv3 PMC "
+                               "(2*FETCH_SIZE + WRITE_SIZE) / algorithmic bytes, committed, "
+                               "times this launch's algorithmic bytes (not measured in this run)")
+            if ratio else None,
             "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}> + pa_merge_kernel",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
     if "beams" in cfg:  # logical bytes: every beam reads its whole context
@@ -369,7 +359,7 @@ def main():
                                                       f"over {world} GPU(s)" if strong else ""),
                        "global_batch": args.global_batch if strong else B * world,
                        "batch_per_gpu": B, "seq_len": T, "page_size": cfg["ts"],
-                       "parallelism": f"batch-sharded x{world} (RCCL logits gather to rank 0)"
+                       "parallelism": f"batch-sharded x{world} (RCCL {args.gather} gather to rank 0)"
                        if not host_gather else f"batch-sharded x{world} ({backend} rehearsal)"},
             "hbm_roofline_frac_step": round(step_b / t_step / 1e9 / HBM_PEAK_GBPS, 4),
             "step_bytes": int(step_b),

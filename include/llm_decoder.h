@@ -398,6 +398,10 @@ int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_width, int sh
 int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
                      int32_t* next_host, void* stream);
 int llm_decoder_sync(llm_decoder* d);
+/* Enqueue on `stream` (NULL: the decoder's) a device copy of the last step's
+ * next ids (int32 [batch], the greedy argmax or the sampled ids) to dst_dev:
+ * the ids-only gather of the multi-GPU path without a host sync. */
+int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* stream);
 /* Activation taps for parity checks (INT8 decoders): every following
  * llm_decoder_step also copies, per layer l and stage s (0: LN1 output, 1:
  * attention output, 2: LN2 output, 3: fc1 output -- the four int8 GEMM inputs

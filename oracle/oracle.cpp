@@ -373,7 +373,37 @@ struct oracle_model {
   const int8_t* wo;   const float* sw_o;       // [L][hid][hid],  [L][hid]
   const int8_t* w1;   const float* sw1; const float* b1;  // [L][hid][inter], [L][inter] x2
   const int8_t* w2;   const float* sw2; const float* b2;  // [L][inter][hid], [L][hid] x2
+  // CUDADecoder (fp16 weights, decoder/cuda_decoder.cu): when hwqkv is set the
+  // four projections use these fp16 [L][K][N] matrices instead of the int8
+  // ones (sw_* unused): y = f16(x) . W in fp32 (+ bias, ReLU for fc1), with
+  // the GEMM inputs rounded to fp16 as the GPU's f16 MFMA consumes them
+  const uint16_t *hwqkv, *hwo, *hw1, *hw2;
 };
+
+// fp16-weight projection of the CUDADecoder restatement: out[m][n] =
+// sum_k f16(x[m][k]) * W[k][n] in fp32 (k order), + bias[n], ReLU if act.
+static void f16_gemm(const float* x, int M, int K, const uint16_t* W, int N, const float* bias,
+                     int act, float* out) {
+#pragma omp parallel
+  {
+    std::vector<float> xr(K);
+#pragma omp for schedule(static)
+    for (int m = 0; m < M; ++m) {
+      for (int k = 0; k < K; ++k) xr[k] = half_to_float(float_to_half(x[(size_t)m * K + k]));
+      float* o = out + (size_t)m * N;
+      for (int n = 0; n < N; ++n) o[n] = 0.0f;
+      for (int k = 0; k < K; ++k) {
+        const float xv = xr[k];
+        const uint16_t* wr = W + (size_t)k * N;
+        for (int n = 0; n < N; ++n) o[n] += xv * half_to_float(wr[n]);
+      }
+      for (int n = 0; n < N; ++n) {
+        float y = o[n] + (bias ? bias[n] : 0.0f);
+        o[n] = act == 1 ? std::max(y, 0.0f) : y;
+      }
+    }
+  }
+}
 
 struct OracleDecoder {
   oracle_model m;
@@ -443,6 +473,8 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
   for (int b = 0; b < B; ++b)
     if (pos[b] < 0 || pos[b] >= m.max_seq || tokens[b] < 0 || tokens[b] >= m.V) return 2;
   const int Lrun = layers_to_run < 0 ? m.L : std::min(layers_to_run, m.L);
+  const bool f16w = m.hwqkv != nullptr;
+  if (f16w && forced_q) return 3;  // teacher forcing is for the int8 activations
   std::vector<float> x((size_t)B * hid), a((size_t)B * hid), qkv((size_t)B * 3 * hid),
       o((size_t)B * hid), h1((size_t)B * inter);
   std::vector<int8_t> qa((size_t)B * std::max(hid, inter));
@@ -478,9 +510,14 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
   for (int l = 0; l < Lrun; ++l) {
     const size_t lh = (size_t)l * hid;
     oracle_layer_norm(x.data(), B, hid, m.ln1_g + lh, m.ln1_b + lh, 1e-5f, a.data());
-    quant(l, 0, a.data(), hid);
-    oracle_i8_gemm(qa.data(), m.wqkv + (size_t)l * hid * 3 * hid, nullptr, qkv.data(), B, 3 * hid,
-                   hid, sa.data(), m.sw_qkv + (size_t)l * 3 * hid, nullptr, 0);
+    if (f16w) {
+      f16_gemm(a.data(), B, hid, m.hwqkv + (size_t)l * hid * 3 * hid, 3 * hid, nullptr, 0,
+               qkv.data());
+    } else {
+      quant(l, 0, a.data(), hid);
+      oracle_i8_gemm(qa.data(), m.wqkv + (size_t)l * hid * 3 * hid, nullptr, qkv.data(), B,
+                     3 * hid, hid, sa.data(), m.sw_qkv + (size_t)l * 3 * hid, nullptr, 0);
+    }
     // KV append (fp16 storage, round to nearest even).
     for (int b = 0; b < B; ++b)
       for (int hh = 0; hh < H; ++hh)
@@ -515,6 +552,14 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
           for (int dd = 0; dd < D; ++dd) ov[dd] += p * half_to_float(vr[dd]);
         }
       }
+    }
+    if (f16w) {
+      f16_gemm(o.data(), B, hid, m.hwo + (size_t)l * hid * hid, hid, nullptr, 0, x.data());
+      oracle_layer_norm(x.data(), B, hid, m.ln2_g + lh, m.ln2_b + lh, 1e-5f, a.data());
+      f16_gemm(a.data(), B, hid, m.hw1 + (size_t)l * hid * inter, inter,
+               m.b1 + (size_t)l * inter, 1, h1.data());
+      f16_gemm(h1.data(), B, inter, m.hw2 + (size_t)l * inter * hid, hid, m.b2 + lh, 0, x.data());
+      continue;
     }
     quant(l, 1, o.data(), hid);
     oracle_i8_gemm(qa.data(), m.wo + (size_t)l * hid * hid, nullptr, x.data(), B, hid, hid,

@@ -31,6 +31,36 @@ def build(force: bool = False) -> None:
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
 
 
+def native_build() -> bool:
+    """Compile liboracle_native.so for the host this runs on (-O3
+    -march=native); False if that fails (bench.py then times the portable
+    build and says so)."""
+    try:
+        subprocess.run(["make", "-s", "-C", str(HERE), "liboracle_native.so"], check=True,
+                       capture_output=True, timeout=300)
+        return True
+    except Exception:
+        return False
+
+
+def host_cpu() -> dict:
+    """CPU model and the cores this process may use (the baseline's `cores`
+    is the OpenMP thread count actually used)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return {"model": model, "cpus_available": avail, "cpus_machine": os.cpu_count()}
+
+
 class OracleModel(ctypes.Structure):
     _fields_ = [
         ("L", ctypes.c_int), ("H", ctypes.c_int), ("D", ctypes.c_int), ("hid", ctypes.c_int),
@@ -41,6 +71,7 @@ class OracleModel(ctypes.Structure):
         ("wo", _i8p), ("sw_o", _f32p),
         ("w1", _i8p), ("sw1", _f32p), ("b1", _f32p),
         ("w2", _i8p), ("sw2", _f32p), ("b2", _f32p),
+        ("hwqkv", _u16p), ("hwo", _u16p), ("hw1", _u16p), ("hw2", _u16p),
     ]
 
 
@@ -52,9 +83,13 @@ def _ptr(a: np.ndarray | None, typ):
 
 
 class Oracle:
-    def __init__(self, bench: bool = False):
+    def __init__(self, bench: bool | str = False):
+        """bench=False: the checker build; True: the portable CPU-baseline
+        build (x86-64-v3); "native": liboracle_native.so (-march=native, built
+        on this host by native_build())."""
         build()
-        name = "liboracle_bench.so" if bench else "liboracle.so"
+        name = ("liboracle_native.so" if bench == "native" else
+                "liboracle_bench.so" if bench else "liboracle.so")
         self.lib = ctypes.CDLL(str(HERE / name))
         L = self.lib
         L.oracle_paged_attention.restype = ctypes.c_int
@@ -184,7 +219,8 @@ class Oracle:
 
 class OracleDecoder:
     """Restated INT8Decoder (contiguous fp16 KV) over host weights (see
-    ``synthetic_int8_model``)."""
+    ``synthetic_int8_model``), or the restated CUDADecoder when the four
+    projection matrices are fp16 (``wqkv`` etc. float16 / uint16 bits)."""
 
     def __init__(self, oracle: Oracle, w: dict, B: int):
         self.o = oracle
@@ -194,10 +230,17 @@ class OracleDecoder:
         m.L, m.H, m.D, m.hid, m.inter, m.V, m.max_seq = (
             cfg["L"], cfg["H"], cfg["D"], cfg["hid"], cfg["inter"], cfg["V"], cfg["max_seq"])
         m.emb = _ptr(w["emb"].view(np.uint16), _u16p)
-        for name in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "sw_qkv", "sw_o", "sw1", "b1", "sw2", "b2"):
+        f16 = w["wqkv"].dtype in (np.float16, np.uint16)  # CUDADecoder weights
+        for name in ("ln1_g", "ln1_b", "ln2_g", "ln2_b", "b1", "b2"):
             setattr(m, name, _ptr(w[name], _f32p))
-        for name in ("wqkv", "wo", "w1", "w2"):
-            setattr(m, name, _ptr(w[name], _i8p))
+        if f16:
+            for name in ("wqkv", "wo", "w1", "w2"):
+                setattr(m, "h" + name, _ptr(np.ascontiguousarray(w[name]).view(np.uint16), _u16p))
+        else:
+            for name in ("sw_qkv", "sw_o", "sw1", "sw2"):
+                setattr(m, name, _ptr(w[name], _f32p))
+            for name in ("wqkv", "wo", "w1", "w2"):
+                setattr(m, name, _ptr(w[name], _i8p))
         self.model = m
         self.B = B
         self.cfg = cfg

@@ -214,6 +214,10 @@ class Decoder {
     py::gil_scoped_release nogil;
     check(llm_decoder_sync(d_));
   }
+  void copy_next_ids(uintptr_t dst, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    check(llm_decoder_copy_next(d_, reinterpret_cast<int32_t*>(dst), reinterpret_cast<void*>(stream)));
+  }
   // llm_decoder_set_taps: device pointers (0, 0 switches the taps off)
   void set_taps(uintptr_t q_ptr, uintptr_t s_ptr) {
     py::gil_scoped_release nogil;
@@ -419,6 +423,7 @@ PYBIND11_MODULE(llm_decoder, m) {
              py::arg("stream") = 0, py::arg("want_next") = true)
         .def("sync", &Decoder::sync)
         .def("set_taps", &Decoder::set_taps, py::arg("q_ptr"), py::arg("s_ptr"))
+        .def("copy_next_ids", &Decoder::copy_next_ids, py::arg("dst_ptr"), py::arg("stream") = 0)
         .def("context_len", &Decoder::context_len)
         .def_property_readonly("kv_handle", &Decoder::kv_handle);
   };

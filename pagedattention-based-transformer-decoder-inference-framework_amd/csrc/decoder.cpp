@@ -91,7 +91,6 @@ struct llm_decoder {
   size_t attn_ws_bytes = 0;
 
   int batch = 0;
-  bool prefill_mfma = true;  // LLM_PREFILL_MFMA=0: prompt chunks through the decode kernel
   std::vector<int> h_pos;  // host mirror of the next position of each row
 
   hipGraphExec_t graph = nullptr;
@@ -106,16 +105,9 @@ struct llm_decoder {
   ~llm_decoder() {
     if (graph) (void)hipGraphExecDestroy(graph);
     if (kv) kv_cache_destroy(kv);
-    for (hipEvent_t e : ev_attn) (void)hipEventDestroy(e);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (stream2) (void)hipStreamDestroy(stream2);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  // micro-batch overlap (see enqueue_step)
-  int microbatches = 1;
-  int mb_attn_waves = 0;  // LLM_MB_ATTN_WAVES: attention waves per SIMD under overlap
   int row_group = 1;  // beam width of llm_decoder_begin_beams (beam-aware attention)
   // sampling (llm_decoder_set_sampling); greedy argmax by default, as the
   // reference's sample_from_logits (decoder/cuda_decoder.cu:7-14)
@@ -123,12 +115,7 @@ struct llm_decoder {
   int top_k = 0;
   float top_p = 1.f;
   uint64_t sample_seed = 0;
-  bool pingpong = true;
-  bool use_graph = true;
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  std::vector<hipEvent_t> ev_attn;  // [L][2]
-  DevBuf<uint8_t> attn_ws2;
+  bool use_graph = true;  // LLM_GRAPH=0: eager launches (per-kernel profiling)
   int qa_ld = 0;
   size_t b16 = 0;  // max_batch rounded up to 16-row tiles
 
@@ -203,38 +190,17 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->ctx.alloc((size_t)B));
   d->pps = 0;  // balanced splits derived on device from each row's context
   d->attn_ws_bytes = 16;
-  for (int b = 1; b <= B; ++b)  // any batch / micro-batch size up to max_batch
+  for (int b = 1; b <= B; ++b)  // any batch size up to max_batch
     d->attn_ws_bytes = std::max(d->attn_ws_bytes,
                                 pa_decode_workspace_bytes(b, d->H, d->D, d->max_tiles, 0));
   RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
   d->qa_ld = std::max(hid, inter);
-  // micro-batch overlap (enqueue_step), off by default: LLM_MICROBATCHES=1|2,
-  // LLM_MB_PINGPONG=0|1, LLM_MB_ATTN_WAVES=n (lean attention under overlap),
-  // LLM_GRAPH=0|1 (eager launches, for profiling).  Measured at C3 (tok/s):
-  // one batch 3607-3621; two free-running halves 3672-3674 (+1.5 %, within
-  // box-to-box spread, and 7 % slower under rocprofv3's kernel trace);
-  // ping-pong attention 3156-3592 — the glue kernels slow 4-8x beside a
-  // saturating KV scan, so the overlap does not pay on this path.  A CU
-  // partition (attention and glue on hipExtStreamCreateWithCUMask streams,
-  // 16/32/48 glue CUs, eager) measured 2485-2645: the weight GEMMs are paced
-  // per CU (~6 GB/s per CU), so 32 CUs need ~275 us of glue per half-layer,
-  // the half-batch scan on 224 CUs runs 9 % slower (365 vs 335 us) and each
-  // cross-stream event adds ~13 us.
-  d->microbatches = env_int("LLM_MICROBATCHES", 1);
-  d->pingpong = env_int("LLM_MB_PINGPONG", 0) != 0;
+  // Overlapping the glue of one half of the rows with the other half's
+  // attention (two micro-batches on two streams, ping-pong ordered) was
+  // measured and removed: 3,672 vs 3,621 tok/s free running, 3,156-3,592
+  // ping-pong (the glue slows 4-8x beside a saturating KV scan), and a CU
+  // partition 2,485-2,645.
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
-  d->prefill_mfma = env_int("LLM_PREFILL_MFMA", 1) != 0;
-  d->mb_attn_waves = env_int("LLM_MB_ATTN_WAVES", 0);
-  if (d->microbatches >= 2 && B >= 2) {
-    LLM_HIP_RET(hipStreamCreateWithFlags(&d->stream2, hipStreamNonBlocking));
-    LLM_HIP_RET(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
-    LLM_HIP_RET(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
-    d->ev_attn.resize((size_t)2 * d->L);
-    for (auto& e : d->ev_attn) LLM_HIP_RET(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    RET_IF(d->attn_ws2.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
-  } else {
-    d->microbatches = 1;
-  }
   d->h_pos.assign(B, 0);
   *out = d.release();
   return LLM_OK;
@@ -337,11 +303,8 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
 // ---------------------------------------------------------------------------
 // step
 // ---------------------------------------------------------------------------
-// Rows [r0, r0 + n) of the batch: every activation / state buffer is
-// row-indexed, so a micro-batch is a set of offset pointers (plus its own
-// attention workspace).
-// The rows one layer pass works on: a decode micro-batch (rows r0.. of the
-// step buffers, one token each) or a prefill chunk (n tokens of one sequence,
+// The rows one layer pass works on: the decode rows (rows r0.. of the step
+// buffers, one token each) or a prefill chunk (n tokens of one sequence,
 // beam_rows[m] = its page-table row).  Every buffer is row-indexed.
 struct Rows {
   int n = 0;
@@ -357,7 +320,6 @@ struct Rows {
   const int32_t* beam_rows = nullptr;  // page-table row per row; NULL: table_row0 + m
   int table_row0 = 0;
   int row_group = 1;
-  int attn_waves_per_simd = 0;  // > 0: lean attention leaving CU room (micro-batch overlap)
   // prefill chunk (row >= 0): the n rows are positions p0 .. p0+n-1 of page-table
   // row prefill_row, attended causally by the MFMA prefill kernel
   int prefill_row = -1;
@@ -369,9 +331,9 @@ struct Rows {
 // Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
 // order (common.hpp a_frag_off_*): their producers (LayerNorm+quant, the
 // attention merge, the row quantiser) write MFMA A-fragments directly, so
-// every GEMM A load is one coalesced 1 KiB read.  Micro-batches start on
-// 16-row boundaries, so a row offset r0 is the same base offset in both
-// layouts (r0 * K elements).
+// every GEMM A load is one coalesced 1 KiB read.  Row offsets r0 are
+// multiples of 16, so r0 is the same base offset in both layouts (r0 * K
+// elements).
 int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   const size_t lh = (size_t)l * hid;
   pa_kv_view view;
@@ -411,9 +373,9 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
-  view.page_table += (size_t)R.table_row0 * H * view.max_tiles;  // rows of this micro-batch
+  view.page_table += (size_t)R.table_row0 * H * view.max_tiles;  // rows r0..
   view.num_beams -= R.table_row0;
-  if (R.prefill_row >= 0 && prefill_mfma && pa_prefill_supported(&view)) {
+  if (R.prefill_row >= 0 && pa_prefill_supported(&view)) {
     // one MFMA pass over the chunk (K/V pages read once per 32 queries), then
     // the o_proj input conversion the decode merge would have fused
     PaRowOutputs ro;
@@ -441,7 +403,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   }
   return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
-                            R.row_group, R.attn_waves_per_simd);
+                            R.row_group, 0);
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
@@ -553,48 +515,16 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
   return LLM_OK;
 }
 
-// One decode step.  With two micro-batches the rows are split in halves that
-// run on two streams (captured as two graph branches); their paged-attention
-// launches are ordered ping-pong (A.attn(l) -> B.attn(l) -> A.attn(l+1) ...), so
-// while one half streams its KV pages the other half's latency-bound glue
-// (LayerNorm, quantisation, weight GEMMs, KV append, split merge) runs beside
-// it instead of between attention launches.
+// One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
-  const int h0 = ((batch + 1) / 2 + 15) / 16 * 16;  // packed-A tiles are 16 rows
-  if (microbatches < 2 || batch < 2 || h0 >= batch) {
-    const Rows R = step_rows(0, batch, attn_ws.p);
-    RET_IF(step_head(st, 0, batch));
-    for (int l = 0; l < L; ++l) {
-      RET_IF(layer_pre(l, st, R));
-      RET_IF(layer_attn(l, st, R));
-      RET_IF(layer_post(l, st, R));
-    }
-    return step_tail(st, 0, batch);
-  }
-  Rows mbs[2] = {step_rows(0, h0, attn_ws.p), step_rows(h0, batch - h0, attn_ws2.p)};
-  mbs[0].attn_waves_per_simd = mbs[1].attn_waves_per_simd = mb_attn_waves;
-  const int r0s[2] = {0, h0};
-  hipStream_t S[2] = {st, stream2};
-  LLM_HIP_RET(hipEventRecord(ev_fork, st));
-  LLM_HIP_RET(hipStreamWaitEvent(stream2, ev_fork, 0));
-  for (int j = 0; j < 2; ++j) RET_IF(step_head(S[j], r0s[j], mbs[j].n));
+  const Rows R = step_rows(0, batch, attn_ws.p);
+  RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
-    for (int j = 0; j < 2; ++j) {
-      RET_IF(layer_pre(l, S[j], mbs[j]));
-      if (pingpong) {
-        // A.attn(l) after B.attn(l-1); B.attn(l) after A.attn(l)
-        if (j == 0 && l > 0) LLM_HIP_RET(hipStreamWaitEvent(S[0], ev_attn[2 * (l - 1) + 1], 0));
-        if (j == 1) LLM_HIP_RET(hipStreamWaitEvent(S[1], ev_attn[2 * l], 0));
-      }
-      RET_IF(layer_attn(l, S[j], mbs[j]));
-      if (pingpong) LLM_HIP_RET(hipEventRecord(ev_attn[2 * l + j], S[j]));
-      RET_IF(layer_post(l, S[j], mbs[j]));
-    }
+    RET_IF(layer_pre(l, st, R));
+    RET_IF(layer_attn(l, st, R));
+    RET_IF(layer_post(l, st, R));
   }
-  for (int j = 0; j < 2; ++j) RET_IF(step_tail(S[j], r0s[j], mbs[j].n));
-  LLM_HIP_RET(hipEventRecord(ev_join, stream2));
-  LLM_HIP_RET(hipStreamWaitEvent(st, ev_join, 0));
-  return LLM_OK;
+  return step_tail(st, 0, batch);
 }
 
 int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host,
@@ -851,6 +781,16 @@ extern "C" int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* lo
   std::lock_guard<std::mutex> g(d->mu);
   hipStream_t st = stream ? as_stream(stream) : d->stream;
   return d->run_step(tokens, logits_dev, next_host, st);
+}
+
+extern "C" int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* stream) {
+  LLM_REQUIRE(d && dst_dev, "llm_decoder_copy_next: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_REQUIRE(d->batch > 0, "llm_decoder_copy_next: no active rows");
+  hipStream_t st = stream ? as_stream(stream) : d->stream;
+  LLM_HIP_RET(hipMemcpyAsync(dst_dev, d->tokens.p, sizeof(int32_t) * d->batch,
+                             hipMemcpyDeviceToDevice, st));
+  return LLM_OK;
 }
 
 extern "C" int llm_decoder_sync(llm_decoder* d) {

@@ -517,6 +517,7 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   return LLM_OK;
 }
 
+#if LLM_TUNING
 // Tuning hook (not in include/llm_decoder.h): i8_gemm with a forced column-tile
 // count, waves per workgroup and rows per workgroup (16 / 32 / 64; 0 = auto).
 // Diagnostic (not in include/llm_decoder.h): i8_gemm_tune with per-workgroup
@@ -581,3 +582,4 @@ extern "C" int i8_gemm_tune(int nt, int waves, int mrows, int a_packed, const in
   hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream), nt, waves, mrows);
   return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune");
 }
+#endif  // LLM_TUNING

@@ -53,7 +53,7 @@ struct LmHeadArgs {
   float* part_val;    // [M][nwg] max per (row, workgroup), or NULL
   int32_t* part_idx;  // [M][nwg]
   int M, V, K, nwg;
-  int mode;  // tuning: bit0 skip MFMA, bit1 skip x staging, bit2 skip E loads
+  int mode;  // 0; tuning build (LLM_LM_MODE): bit0 skip MFMA, bit1 skip x staging, bit2 skip E loads
 };
 
 // MT = 16-row tiles of x per workgroup (1, 2 or 4).
@@ -267,10 +267,14 @@ hipError_t launch_lm_pack(const void* E, void* P, int V, int K, hipStream_t st) 
 
 hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, int V, int K,
                           float* part_val, int32_t* part_idx, hipStream_t st) {
+#if LLM_TUNING
   static const int mode = [] {
     const char* v = std::getenv("LLM_LM_MODE");
     return v ? std::atoi(v) : 0;
   }();
+#else
+  constexpr int mode = 0;
+#endif
   LmHeadArgs a{x, static_cast<const _Float16*>(E), logits, part_val, part_idx, M, V, K,
                lm_head_workgroups(V), mode};
   const int mt = M <= 16 ? 1 : M <= 32 ? 2 : 4;

@@ -951,15 +951,19 @@ int llm::pa_merge_rows_internal(const float* part_acc, const float* part_ml, flo
 
 namespace {
 // Cost of a beam-private tile relative to a shared one, in 1/16ths (beam-group
-// launches, dynamic splits).  LLM_BEAM_BALANCE16 overrides it (0: equal tile
-// counts, the plain partition) for tuning.
+// launches, dynamic splits).  In the tuning build (make tune) LLM_BEAM_BALANCE16
+// overrides it (0: equal tile counts, the plain partition).
 int beam_balance16() {
+#if LLM_TUNING
   static const int v = [] {
     const char* e = std::getenv("LLM_BEAM_BALANCE16");
     const int x = e ? std::atoi(e) : 44;
     return x >= 16 ? x : 0;
   }();
   return v;
+#else
+  return 44;  // measured sweep in DESIGN.md §8 (C4 launch 84 -> 66 us)
+#endif
 }
 
 // Resident waves of the beam-group kernel (0 where the plain schedule runs
@@ -1137,6 +1141,7 @@ extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
                             pages_per_split, workspace, workspace_bytes, as_stream(stream));
 }
 
+#if LLM_TUNING
 // Tuning hook (not part of include/llm_decoder.h): run the split kernel of
 // D=128 / TS=16 in a given variant so scripts/bench_kernels.py can compare
 // register-stage sizes and cache policies in one process.
@@ -1190,3 +1195,4 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
   LLM_HIP_RET(hipGetLastError());
   return LLM_OK;
 }
+#endif  // LLM_TUNING

@@ -291,7 +291,11 @@ struct PrefillPlan {
 };
 PrefillPlan prefill_plan(const pa_kv_view* kv, int p0, int m) {
   PrefillPlan p;
+#if LLM_TUNING
   p.nw = env_int("LLM_PREFILL_NW", 4) == 2 ? 2 : 4;
+#else
+  p.nw = 4;
+#endif
   const int TS = kv->page_size;
   const int step = kKeyBlock / TS;  // tiles per key block
   const int ntiles = (p0 + m + TS - 1) / TS;

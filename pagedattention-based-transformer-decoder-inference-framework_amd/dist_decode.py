@@ -4,15 +4,20 @@ The reference is single-GPU, batch 1 (decoder/decoder_block.hpp:48); there is
 no collective anywhere in it.  Decode rows are independent, so the multi-GPU
 design shards SEQUENCES across ranks (each rank owns its rows' KV pages and a
 full weight replica) and exchanges nothing inside a step.  The one collective
-is the gather of each step's final logits (or of the generated ids) to rank 0
-over RCCL (`backend="nccl"` is RCCL on ROCm), which receives from every peer
-over its own xGMI link.
+is the gather of each step's output to rank 0 over RCCL (`backend="nccl"` is
+RCCL on ROCm): either the final logits ([rows][V] fp32, 12.9 MB per 64-row
+shard) or, for greedy decoding, only the argmax ids ([rows] int32).
+Rank 0 receives from every peer on its own xGMI link.
 
-Device-agnostic: the same code runs with the gloo backend on CPU tensors,
-which is how tests/test_dist_gloo.py exercises it at world_size 2.
+This module is THE multi-rank decode loop: bench.py times it on the GPU ranks
+(HipDecoderStep over the HIP decoder) and tests/test_dist_gloo.py runs the
+same code with the gloo backend on CPU tensors (an oracle-backed step) at world
+sizes 2 and 4, weak and strong (ragged) sharding, bit-exact against one
+process.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable, Sequence
 
 
@@ -27,12 +32,17 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return lo, hi
 
 
-class LogitsGatherer:
-    """Double-buffered asynchronous gather of per-step logits to rank 0.
+def shard_sizes(n: int, world: int) -> list[int]:
+    return [hi - lo for lo, hi in (shard_range(n, world, r) for r in range(world))]
+
+
+class RowGatherer:
+    """Double-buffered asynchronous gather of per-step row outputs (logits
+    [rows][V] or ids [rows]) to rank 0.
 
     Per step: t = buffer() (waits for the gather that last used this slot),
-    write the step's logits into t, push().  A slot is re-used only after its
-    previous gather completed, so step s+1 computes while step s's logits move.
+    write the step's rows into t, push().  A slot is re-used only after its
+    previous gather completed, so step s+1 computes while step s's rows move.
     With keep=True rank 0 accumulates every gathered step (per-rank tensors
     concatenated along rows) in `completed`, in step order."""
 
@@ -40,7 +50,8 @@ class LogitsGatherer:
                  keep: bool = False):
         import torch
         self.world, self.rank, self.keep = world, rank, keep
-        rows = shard_rows or [shape[0]] * world
+        rows = list(shard_rows) if shard_rows else [shape[0]] * world
+        self.equal = len(set(rows)) == 1
         self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(2)]
         self.recv = [[torch.empty((rows[r],) + tuple(shape[1:]), dtype=dtype, device=device)
                       for r in range(world)] if rank == 0 else None for _ in range(2)]
@@ -58,14 +69,14 @@ class LogitsGatherer:
                 self.completed.append(torch.cat(self.recv[s]).clone())
 
     def buffer(self):
-        """The tensor the next step should write its logits into."""
+        """The tensor the next step should write its rows into."""
         self._retire(self.slot)
         return self.bufs[self.slot]
 
     def push(self):
         s = self.slot
         if self.world > 1:
-            self.works[s] = _gather(self.bufs[s], self.recv[s], self.rank)
+            self.works[s] = _gather(self.bufs[s], self.recv[s], self.rank, self.equal)
         elif self.keep:
             self.completed.append(self.bufs[s].clone())
         self.slot ^= 1
@@ -77,18 +88,23 @@ class LogitsGatherer:
         return self.completed
 
 
-def _gather(t, recv, rank):
-    """gather with unequal shard sizes: point-to-point receives on rank 0 (each
-    peer on its own link), a single send elsewhere."""
+LogitsGatherer = RowGatherer  # the name of the round-1 API
+
+
+def _gather(t, recv, rank, equal):
+    """Equal shards: one torch.distributed gather.  Unequal (ragged strong
+    scaling): point-to-point receives on rank 0, each peer on its own link, and
+    a single send elsewhere."""
     import torch.distributed as dist
+    if equal:
+        return dist.gather(t, recv if rank == 0 else None, dst=0, async_op=True)
     world = dist.get_world_size()
     if rank == 0:
         recv[0].copy_(t)
         ops = [dist.P2POp(dist.irecv, recv[r], r) for r in range(1, world)]
     else:
         ops = [dist.P2POp(dist.isend, t, 0)]
-    reqs = dist.batch_isend_irecv(ops)
-    return _Works(reqs)
+    return _Works(dist.batch_isend_irecv(ops))
 
 
 class _Works:
@@ -98,6 +114,101 @@ class _Works:
     def wait(self):
         for r in self.reqs:
             r.wait()
+
+
+class HipDecoderStep:
+    """One decode step of an llm_decoder INT8Decoder / CUDADecoder on a HIP
+    stream: logits (if asked) go to a device tensor, greedy ids to an int32
+    device tensor, without a host synchronisation."""
+
+    def __init__(self, dec, stream=None):
+        import torch
+        self.dec = dec
+        self.sp = (stream or torch.cuda.current_stream()).cuda_stream
+
+    def __call__(self, tokens, logits_out):
+        self.dec.step(tokens, logits_ptr=logits_out.data_ptr() if logits_out is not None else 0,
+                      stream=self.sp, want_next=False)
+
+    def ids_into(self, out):
+        self.dec.copy_next_ids(out.data_ptr(), self.sp)
+
+
+class ShardedDecode:
+    """This rank's part of a batch-sharded decode: `step_fn` decodes the rank's
+    `rows` (step_fn(tokens or None, logits_out or None); step_fn.ids_into(t)
+    for gather="ids"), and each step's output goes to rank 0.
+
+    gather: "logits" (the step's [rows][V] fp32 logits), "ids" (the greedy
+    next ids, int32 [rows]) or "none".  A single rank gathers nothing unless
+    keep=True.  staging="host" copies each step's output to host memory
+    before the gather (a gloo rehearsal of the GPU path)."""
+
+    def __init__(self, step_fn, rows: int, vocab: int, *, world: int = 1, rank: int = 0,
+                 shard_rows: Sequence[int] | None = None, gather: str = "logits",
+                 device="cuda", staging: str = "device", keep: bool = False):
+        import torch
+        if gather not in ("logits", "ids", "none"):
+            raise ValueError("gather must be 'logits', 'ids' or 'none'")
+        self.step_fn, self.world, self.rank, self.gather = step_fn, world, rank, gather
+        self.active = gather != "none" and (world > 1 or keep)
+        self.host = staging == "host"
+        shape, dtype = ((rows, vocab), torch.float32) if gather == "logits" else ((rows,), torch.int32)
+        gdev = "cpu" if self.host else device
+        self.dev_buf = torch.empty(shape, dtype=dtype, device=device) if self.host else None
+        self.g = RowGatherer(shape, dtype, gdev, world, rank, shard_rows, keep) if self.active else None
+
+    def step(self, tokens=None):
+        if not self.active:
+            self.step_fn(tokens, None)
+            return
+        buf = self.g.buffer()
+        out = self.dev_buf if self.host else buf
+        if self.gather == "logits":
+            self.step_fn(tokens, out)
+        else:
+            self.step_fn(tokens, None)
+            self.step_fn.ids_into(out)
+        if self.host:
+            buf.copy_(out)
+        self.g.push()
+
+    def finish(self):
+        return self.g.finish() if self.g else []
+
+
+def timed_run(sd: ShardedDecode, warmup: int, steps: int, first_tokens, *,
+              sync: Callable[[], None] | None = None, timer_device="cuda") -> float:
+    """bench.py's measured loop: `warmup` untimed steps (the first feeds
+    first_tokens, later steps feed back the device's ids), then exactly `steps`
+    timed ones bracketed by a barrier + device synchronisation on both sides.
+    Returns the elapsed seconds, the MAX over ranks."""
+    import torch
+    import torch.distributed as dist
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    if sync is None:
+        sync = torch.cuda.synchronize
+    for i in range(warmup):
+        sd.step(first_tokens if i == 0 else None)
+    sd.finish()
+    sync()
+    if multi:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        sd.step(first_tokens if warmup == 0 and i == 0 else None)
+    sd.finish()
+    sync()
+    if multi:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if multi:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=timer_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def distributed_generate(make_decoder: Callable, prompts: Sequence[Sequence[int]],

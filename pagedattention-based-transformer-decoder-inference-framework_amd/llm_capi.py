@@ -17,6 +17,7 @@ from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "libllm_decoder_hip.so"
+TUNE_LIB_PATH = HERE / "libllm_decoder_hip_tune.so"  # `make tune`: A/B hooks, never the product
 
 LLM_OK, LLM_ERR_INVALID, LLM_ERR_UNSUPPORTED, LLM_ERR_HIP, LLM_ERR_OOM, LLM_ERR_IO = range(6)
 LLM_F16, LLM_I8, LLM_F32, LLM_BF16 = 0, 1, 2, 3
@@ -147,9 +148,29 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
     return lib
 
 
-def check(status: int) -> None:
+_tune = None
+
+
+def load_tune() -> ctypes.CDLL:
+    """The tuning build (pa_decode_tune, i8_gemm_tune, i8_gemm_stamps and the
+    env overrides), loaded RTLD_LOCAL beside the product library; for scripts
+    and the variant tests only."""
+    global _tune
+    if _tune is None:
+        if not TUNE_LIB_PATH.exists():
+            raise FileNotFoundError(f"{TUNE_LIB_PATH} not found: `make -C {HERE} tune`")
+        _tune = ctypes.CDLL(str(TUNE_LIB_PATH), mode=ctypes.RTLD_LOCAL)
+        for name, (res, args) in _SIGS.items():
+            if hasattr(_tune, name):
+                f = getattr(_tune, name)
+                f.restype = res
+                f.argtypes = args
+    return _tune
+
+
+def check(status: int, lib: ctypes.CDLL | None = None) -> None:
     if status != LLM_OK:
-        msg = load().llm_last_error()
+        msg = (lib or load()).llm_last_error()
         raise LlmError(status, msg.decode() if msg else "")
 
 

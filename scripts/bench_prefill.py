@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Prefill attention: the MFMA chunk kernel (pa_prefill) against the same rows
 through the decode kernel (pa_decode with beam_ids = row, context_lens =
-p0 + i + 1), and a whole-decoder prompt prefill with LLM_PREFILL_MFMA=1 / 0.
+p0 + i + 1), and a whole-decoder prompt prefill (MFMA prefill kernel).
 
     python scripts/bench_prefill.py [--p0 7680] [--m 512] [--prompt 4096]
 
@@ -60,11 +60,10 @@ def kernel_bench(H, D, ts, p0, m):
             "kv_unique_GB": round(2 * H * T * D * 2 / 1e9, 4)}
 
 
-def decoder_bench(prompt, mfma):
+def decoder_bench(prompt):
     import llm_decoder
     from bench import CONFIGS, make_weights
     cfg = CONFIGS["c3"]
-    os.environ["LLM_PREFILL_MFMA"] = "1" if mfma else "0"
     hid = cfg["H"] * cfg["D"]
     dec = llm_decoder.INT8Decoder(cfg["L"], cfg["H"], cfg["D"], hid, cfg["V"], prompt + 64,
                                   max_batch=1, page_size=cfg["ts"])
@@ -95,13 +94,10 @@ def main():
                       kernel_bench(16, 128, 16, 0, args.m),
                       kernel_bench(12, 64, 16, 1536, args.m)]}
     if not args.no_decoder:
-        t1 = decoder_bench(args.prompt, True)
-        t0 = decoder_bench(args.prompt, False)
+        t1 = decoder_bench(args.prompt)
         res["decoder"] = {"config": "C3 dims (24L/16H/D128, INT8), batch 1",
                           "prompt_tokens": args.prompt, "mfma_prefill_s": round(t1, 3),
-                          "decode_kernel_prefill_s": round(t0, 3),
-                          "mfma_prompt_tok_per_s": round(args.prompt / t1, 1),
-                          "speedup": round(t0 / t1, 2)}
+                          "mfma_prompt_tok_per_s": round(args.prompt / t1, 1)}
     print(json.dumps(res), flush=True)
 
 

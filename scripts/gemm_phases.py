@@ -20,7 +20,7 @@ ap.add_argument("--hid", type=int, default=2048)
 ap.add_argument("--diag", type=int, nargs="*", default=[0],
                 help="0 full kernel, 1 no A loads, 2 no epilogue, 3 both")
 args = ap.parse_args()
-lib = llm_capi.load()
+lib = llm_capi.load_tune()  # tuning build: `make tune`
 lib.i8_gemm_stamps.restype = ctypes.c_int
 lib.i8_gemm_stamps.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + \
     [ctypes.c_void_p] * 5

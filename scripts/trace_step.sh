@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-trace one bench configuration (env passed through) for timeline analysis.
-#   bash scripts/trace_step.sh NAME [extra bench.py args]   (env: LLM_MICROBATCHES, LLM_MB_PINGPONG, LLM_GRAPH)
+#   bash scripts/trace_step.sh NAME [extra bench.py args]   (env: LLM_GRAPH=0 for eager launches)
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT

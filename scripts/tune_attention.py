@@ -59,7 +59,7 @@ if args.extent > 1 and not args.interleave:
     assert nt % ext == 0
     runs = torch.randperm(num_pages // ext, generator=g, device="cuda").to(torch.int32)
     pt = (runs[:, None] * ext + torch.arange(ext, device="cuda", dtype=torch.int32)).reshape(B, H, nt)
-lib = llm_capi.load()
+lib = llm_capi.load_tune()  # tuning build: `make tune`
 lib.pa_decode_tune.restype = ctypes.c_int
 lib.pa_decode_tune.argtypes = [ctypes.c_int, ctypes.POINTER(llm_capi.PaKvView), ctypes.c_void_p,
                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,

@@ -18,7 +18,7 @@ ap.add_argument("--M", type=int, default=64)
 ap.add_argument("--reps", type=int, default=50)
 ap.add_argument("--hid", type=int, default=2048)
 args = ap.parse_args()
-lib = llm_capi.load()
+lib = llm_capi.load_tune()  # tuning build: `make tune`
 lib.i8_gemm_tune.restype = ctypes.c_int
 lib.i8_gemm_tune.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                              ctypes.c_int,

@@ -1,6 +1,10 @@
-"""N > 1 path on CPU: world_size-2 gloo processes shard the rows, step the
-(oracle) decoder on their shard and gather logits / generated ids to rank 0;
-rank 0's result must equal a single-process run over all rows bit-exactly."""
+"""N > 1 path on CPU: gloo processes run bench.py's multi-rank decode loop
+(dist_decode.ShardedDecode + timed_run) over an oracle-backed step, at world
+sizes 2 and 4, with weak scaling (a fixed batch per rank, as the default bench
+line) and ragged strong scaling (--global-batch G sharded with shard_range),
+gathering logits or greedy ids to rank 0.  Rank 0's gathered
+steps must equal a single-process run over all rows bit for bit.  The same
+loop runs on the GPU ranks with HipDecoderStep over RCCL (unmeasured here)."""
 import os
 import socket
 import sys
@@ -11,6 +15,7 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 PKG = ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"
+WARMUP, STEPS, ROWS_PER_RANK = 2, 3, 3
 
 
 def _free_port():
@@ -25,6 +30,72 @@ def _model():
     from oracle.oracle import Oracle, synthetic_int8_model
     o = Oracle()
     return o, synthetic_int8_model(o, L=2, H=2, D=64, V=300, max_seq=32, seed=21)
+
+
+class _OracleStep:
+    """A step_fn for ShardedDecode over the oracle decoder: every row one token
+    per step at its own position; tokens=None feeds back the greedy ids, as
+    llm_decoder_step(tokens=NULL) does on the GPU."""
+
+    def __init__(self, o, w, n):
+        from oracle.oracle import OracleDecoder
+        self.dec = OracleDecoder(o, w, n)
+        self.n, self.pos, self.next = n, 0, None
+
+    def __call__(self, tokens, logits_out):
+        import torch
+        tok = np.asarray(tokens if tokens is not None else self.next, np.int32)
+        _, logits, nxt = self.dec.step(tok, np.full(self.n, self.pos, np.int32))
+        self.pos += 1
+        self.next = nxt
+        if logits_out is not None:
+            logits_out.copy_(torch.from_numpy(logits))
+
+    def ids_into(self, out):
+        import torch
+        out.copy_(torch.from_numpy(self.next))
+
+
+def _tokens(mode, world, rank, global_rows):
+    """First-step tokens of this rank, as bench.py draws them (weak: one draw
+    per rank seed; strong: one global draw, sharded)."""
+    from dist_decode import shard_range
+    if mode == "weak":
+        return np.random.default_rng(1234 + rank).integers(0, 300, ROWS_PER_RANK).astype(np.int32)
+    lo, hi = shard_range(global_rows, world, rank)
+    return np.random.default_rng(1234).integers(0, 300, global_rows).astype(np.int32)[lo:hi]
+
+
+def _worker(rank, world, port, mode, gather, staging, global_rows, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (str(ROOT), str(PKG)):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import dist_decode
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o, w = _model()
+    shard_rows = None
+    if mode == "weak":
+        rows = ROWS_PER_RANK
+    else:
+        shard_rows = dist_decode.shard_sizes(global_rows, world)
+        rows = shard_rows[rank]
+    sd = dist_decode.ShardedDecode(_OracleStep(o, w, rows), rows, w["cfg"]["V"], world=world,
+                                   rank=rank, shard_rows=shard_rows, gather=gather,
+                                   device="cpu", staging=staging, keep=True)
+    first = [int(t) for t in _tokens(mode, world, rank, global_rows)]
+    elapsed = dist_decode.timed_run(sd, WARMUP, STEPS, first, sync=lambda: None,
+                                    timer_device="cpu")
+    collected = [t.numpy() for t in sd.finish()]
+    gen = None
+    if mode == "weak" and gather == "logits":  # distributed_generate over the same group
+        rng = np.random.default_rng(0)
+        prompts = [[int(x) for x in rng.integers(0, 300, n)] for n in (3, 1, 4, 2, 5)]
+        gen = (prompts, dist_decode.distributed_generate(lambda n: _OracleGen(o, w, n), prompts, 4))
+    if rank == 0:
+        q.put((collected, elapsed, gen))
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 class _OracleGen:
@@ -49,67 +120,48 @@ class _OracleGen:
         return res
 
 
-def _worker(rank, world, port, rows, steps, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    for p in (str(ROOT), str(PKG)):
-        sys.path.insert(0, p)
-    import torch
-    import torch.distributed as dist
-    from dist_decode import LogitsGatherer, distributed_generate, shard_range
-    from oracle.oracle import OracleDecoder
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    o, w = _model()
-    lo, hi = shard_range(rows, world, rank)
-    dec = OracleDecoder(o, w, hi - lo)
-    sizes = [shard_range(rows, world, r)[1] - shard_range(rows, world, r)[0] for r in range(world)]
-    g = LogitsGatherer((hi - lo, w["cfg"]["V"]), torch.float32, "cpu", world, rank, sizes,
-                       keep=True)
-    rng = np.random.default_rng(0)
-    all_toks = rng.integers(0, w["cfg"]["V"], (steps, rows)).astype(np.int32)
-    for s in range(steps):
-        buf = g.buffer()
-        _, logits, _ = dec.step(all_toks[s, lo:hi], np.full(hi - lo, s, np.int32))
-        buf.copy_(torch.from_numpy(logits))
-        g.push()
-    collected = [t.numpy() for t in g.finish()]
-    prompts = [[int(x) for x in rng.integers(0, 300, n)] for n in (3, 1, 4, 2, 5)]
-    gen = distributed_generate(lambda n: _OracleGen(o, w, n), prompts, 4)
-    if rank == 0:
-        q.put((collected, gen, all_toks, prompts))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", [2, 4])
-def test_two_rank_gloo_shard_and_gather(world):
-    """world 2 (the N > 1 path) and world 4 (ragged shards: 5 rows as 2/1/1/1)."""
+@pytest.mark.parametrize("world,mode,gather,staging,global_rows", [
+    (2, "weak", "logits", "device", 0),
+    (4, "weak", "ids", "host", 0),
+    (2, "strong", "ids", "device", 5),     # ragged: 3 + 2
+    (4, "strong", "logits", "host", 7),    # ragged: 2 + 2 + 2 + 1
+    (4, "strong", "logits", "device", 8),  # equal shards: one collective gather
+])
+def test_sharded_decode_loop_matches_single_process(world, mode, gather, staging, global_rows):
     import torch.multiprocessing as mp
-    rows, steps = 5, 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, rows, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, mode, gather, staging, global_rows, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    collected, gen, all_toks, prompts = q.get(timeout=240)
+    collected, elapsed, gen = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single-process reference over all rows
-    from oracle.oracle import OracleDecoder
+    assert elapsed > 0
+    # single process over all rows, the rows in rank order
     o, w = _model()
-    ref = OracleDecoder(o, w, rows)
-    assert len(collected) == steps
-    for s in range(steps):
-        _, logits, _ = ref.step(all_toks[s], np.full(rows, s, np.int32))
-        np.testing.assert_array_equal(collected[s], logits)
-    ref_gen = _OracleGen(o, w, len(prompts)).generate_batch(prompts, 4)
-    assert gen == ref_gen
+    first = np.concatenate([_tokens(mode, world, r, global_rows) for r in range(world)])
+    n = len(first)
+    ref = _OracleStep(o, w, n)
+    assert len(collected) == WARMUP + STEPS
+    for s in range(WARMUP + STEPS):
+        import torch
+        out = torch.empty((n, w["cfg"]["V"]), dtype=torch.float32)
+        ref([int(t) for t in first] if s == 0 else None, out)
+        want = out.numpy() if gather == "logits" else ref.next
+        np.testing.assert_array_equal(collected[s], want)
+    if gen is not None:
+        prompts, got = gen
+        assert got == _OracleGen(o, w, len(prompts)).generate_batch(prompts, 4)
 
 
 def test_shard_range_covers_batch():
     sys.path.insert(0, str(PKG))
-    from dist_decode import shard_range
+    from dist_decode import shard_range, shard_sizes
     for n in (0, 1, 5, 64, 512, 513):
         for world in (1, 2, 3, 8):
             spans = [shard_range(n, world, r) for r in range(world)]
@@ -117,3 +169,4 @@ def test_shard_range_covers_batch():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             sizes = [b - a for a, b in spans]
             assert max(sizes) - min(sizes) <= 1
+            assert shard_sizes(n, world) == sizes

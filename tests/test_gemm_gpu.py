@@ -61,12 +61,13 @@ def test_i8_gemm_no_scales(gpu, oracle):
 ])
 def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
     """The decoder's GEMM form: A in packed-A (MFMA fragment) order, forced
-    column-tile count / waves per workgroup (exported tuning entry
-    i8_gemm_tune): bit-exact against the oracle like the row-major C ABI."""
+    column-tile count / waves per workgroup (i8_gemm_tune of the tuning build,
+    `make tune`: the same kernels): bit-exact against the oracle like the
+    row-major C ABI."""
     import ctypes
     import torch
     import llm_capi
-    lib = llm_capi.load()
+    lib = llm_capi.load_tune()
     lib.i8_gemm_tune.restype = ctypes.c_int
     lib.i8_gemm_tune.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                                       ctypes.c_void_p] + [ctypes.c_int] * 3 + \
@@ -85,7 +86,7 @@ def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
             C = torch.full((M, N), float("nan"), device="cuda")
             llm_capi.check(lib.i8_gemm_tune(nt, waves, mrows, packed, a_t.data_ptr(), K,
                                             Wp.data_ptr(), C.data_ptr(), M, N, K, dsa.data_ptr(),
-                                            dsw.data_ptr(), None))
+                                            dsw.data_ptr(), None), lib)
             np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
 
 

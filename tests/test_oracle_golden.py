@@ -178,3 +178,19 @@ def test_oracle_decoder_step_consistent(oracle):
     ref_logits = xx.astype(np.float64) @ w["emb"].astype(np.float64).T
     assert rel_err(logits, ref_logits) < 1e-4
     np.testing.assert_array_equal(nxt, np.argmax(logits, axis=1))
+
+
+def test_oracle_under_address_sanitizer():
+    """The checker itself is memory-clean: oracle.cpp built with
+    -fsanitize=address,undefined and driven over ragged shapes, missing and
+    out-of-pool pages, filters and the (teacher-forced) decoder step
+    (oracle/asan_check.cpp, `make -C oracle asan`)."""
+    import shutil
+    import subprocess
+    from pathlib import Path
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    root = Path(__file__).resolve().parents[1]
+    r = subprocess.run(["make", "-s", "-C", str(root / "oracle"), "asan"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0 and "asan_check: ok" in r.stdout, r.stdout + r.stderr
