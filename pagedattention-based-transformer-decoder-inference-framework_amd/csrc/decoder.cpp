@@ -101,6 +101,8 @@ struct llm_decoder {
   int8_t* tap_q = nullptr;
   float* tap_s = nullptr;
   int tap(int l, int stage, const struct Rows& R, int K, hipStream_t st);
+  int layer_norm_into(WeightGemm& g, const struct Rows& R, const float* gamma, const float* beta,
+                      hipStream_t st);
 
   ~llm_decoder() {
     if (graph) (void)hipGraphExecDestroy(graph);
@@ -359,15 +361,29 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   g.M = R.n; g.N = 3 * hid; g.K = hid;
   g.C = R.q; g.c_cols = hid; g.c_ld = hid;  // q only: K and V go straight into the pages
   g.kv = &app;
-  if (wdtype == LLM_I8) {
-    LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, nullptr,
-                                       static_cast<int8_t*>(R.act), R.sa, st, 1));
-    RET_IF(tap(l, 0, R, hid, st));
-    g.sa = R.sa; g.sw = sw_qkv.p + (size_t)l * 3 * hid;
-  } else {
-    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln1_g.p + lh, ln1_b.p + lh, 1e-5f, R.act, st, 1));
+  if (wdtype == LLM_I8) g.sa = R.sa, g.sw = sw_qkv.p + (size_t)l * 3 * hid;
+  RET_IF(layer_norm_into(g, R, ln1_g.p + lh, ln1_b.p + lh, st));
+  RET_IF(weight_gemm(g, st));
+  return tap(l, 0, R, hid, st);
+}
+
+// LN(x) as the GEMM's A: fused into the GEMM as its LayerNorm prologue when
+// the rows' A image fits in LDS (decode rows), else a LayerNorm (+ quant)
+// launch writing the packed A the GEMM reads.
+int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamma,
+                                 const float* beta, hipStream_t st) {
+  static const int fuse = env_int("LLM_LN_FUSE", 1);  // TEMP A/B knob
+  if (fuse && R.prefill_row < 0 && ln_fusable(wdtype, R.n, hid)) {
+    g.ln_x = R.x; g.ln_g = gamma; g.ln_b = beta; g.ln_eps = 1e-5f;
+    if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
+    return LLM_OK;
   }
-  return weight_gemm(g, st);
+  if (wdtype == LLM_I8)
+    LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, gamma, beta, 1e-5f, nullptr,
+                                       static_cast<int8_t*>(R.act), R.sa, st, 1));
+  else
+    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, gamma, beta, 1e-5f, R.act, st, 1));
+  return LLM_OK;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
@@ -420,12 +436,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
   RET_IF(weight_gemm(g, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
-  if (i8) {
-    LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, nullptr,
-                                       static_cast<int8_t*>(R.act), R.sa, st, 1));
-    RET_IF(tap(l, 2, R, hid, st));
-  } else
-    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, ln2_g.p + lh, ln2_b.p + lh, 1e-5f, R.act, st, 1));
+  RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
   if (i8) {
@@ -438,6 +449,8 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
     g.C16 = R.act2;
   }
   RET_IF(weight_gemm(g, st));
+  if (i8) RET_IF(tap(l, 2, R, hid, st));
+  g.ln_x = nullptr; g.act_out = nullptr; g.sa_out = nullptr;
   g.C16 = nullptr;
   if (!i8) g.A = R.act2;
   // quantise h1 -> mlp_fc2 (+b2)

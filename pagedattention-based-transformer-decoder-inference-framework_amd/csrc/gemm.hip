@@ -24,6 +24,7 @@
 //     row = 4*(lane>>4) + reg (cdna_hip_programming.md §3).
 #include "common.hpp"
 #include "gemm.hpp"
+#include "ln_wave.hpp"
 
 namespace llm {
 
@@ -58,7 +59,24 @@ struct GemmArgs {
   _Float16* c16;      // optional fp16 copy of C in packed-A order (the next GEMM's input)
   KvAppend kv;        // kv.k_pool == nullptr: no append
   unsigned long long* stamps;  // diagnostics only (i8_gemm_stamps): per-workgroup phase clocks
+  // LayerNorm prologue (gemm_kernel<..., PRO = 1>): A = LN(ln_x) (I8: quantised
+  // per row, scales kept in LDS for the epilogue), computed by every workgroup
+  // for its own rows into LDS instead of read from a LayerNorm launch's output
+  const float* ln_x;      // [M][K] fp32
+  const float* ln_g;      // [K]
+  const float* ln_b;      // [K]
+  float ln_eps;
+  uint8_t* act_out;       // optional: workgroups with blockIdx.x == 0 store A (packed-A order)
+  float* sa_out;          //   and the I8 row scales (activation taps)
 };
+
+// LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
+// stride K * ESIZE + 32 bytes.  With that stride (K * ESIZE a multiple of 256)
+// a wave writing one row is conflict-free (8 consecutive lanes = 128
+// contiguous bytes) and the fragment read of a k-step (lane l: row l & 15,
+// group 4 ks + (l >> 4)) puts every 16-lane ds_read_b128 group on 16
+// distinct 16-byte slots (slot = 2 row + group mod 16).
+__host__ __device__ constexpr int ln_row_stride(int K, int esize) { return K * esize + 32; }
 
 // Phase clock (100 MHz s_memrealtime) of the diagnostic build path.
 __device__ __forceinline__ unsigned long long phase_clock() {
@@ -108,7 +126,61 @@ struct GemmTraits<GemmKind::F16> {
 // Weight loads are non-temporal (each weight byte is read once per step).
 // DIAG (diagnostics only, i8_gemm_stamps): bit 0 = no A loads (A reads as
 // zero), bit 1 = no epilogue (wave 0 stores one word per workgroup).
-template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0>
+// LayerNorm (+ int8 quantisation) of this workgroup's ROWS rows of ln_x into
+// the LDS image of A (ln_row_stride) and, for I8, the row scales into sa_lds:
+// ln_wave.hpp, bit-identical to the LayerNorm launch.  One wave per row (rows
+// w, w + WAVES, ...), two rows' loads in flight; gamma / beta loaded once.
+template <GemmKind KIND, int ROWS, int WAVES>
+__device__ __forceinline__ void ln_prologue(const GemmArgs& a, int m0, uint8_t* alds,
+                                            float* sa_lds) {
+  constexpr int ESIZE = GemmTraits<KIND>::ESIZE;
+  constexpr int CPL = 8;  // float4 chunks per lane (K <= 2048, ln_fusable)
+  const int lane = lane_id();
+  const int w = wave_id_uniform();
+  const int K = a.K;
+  const int K4 = K >> 2;
+  const int stride = ln_row_stride(K, ESIZE);
+  LnRow<CPL> gm, bt;
+  ln_wave_load(a.ln_g, K4, true, gm);
+  ln_wave_load(a.ln_b, K4, true, bt);
+  for (int r0 = w; r0 < ROWS; r0 += 2 * WAVES) {
+    LnRow<CPL> x[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = r0 + q * WAVES;
+      const int m = m0 + r;
+      ln_wave_load(a.ln_x + (size_t)m * K, K4, r < ROWS && m < a.M, x[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int r = r0 + q * WAVES;
+      if (r >= ROWS) break;
+      const bool mok = m0 + r < a.M;  // rows past M: zero A (their outputs are not stored)
+      const float am = ln_wave_compute(x[q], gm, bt, K, a.ln_eps);
+      uint8_t* rowp = alds + (size_t)r * stride;
+      if constexpr (KIND == GemmKind::I8) {
+        const float scale = 127.f / (am + 1e-6f);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const int c = 64 * j + lane;  // consecutive lanes, consecutive dwords
+          if (c < K4)
+            *reinterpret_cast<uint32_t*>(rowp + 4 * c) = mok ? ln_quant4(x[q].v[j], scale) : 0u;
+        }
+        if (lane == 0) sa_lds[r] = mok ? 1.0f / scale : 0.f;
+      } else {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          const int c = 64 * j + lane;
+          if (c < K4)
+            *reinterpret_cast<ln_f16x4*>(rowp + 8 * c) =
+                mok ? ln_half4(x[q].v[j]) : ln_f16x4{0, 0, 0, 0};
+        }
+      }
+    }
+  }
+}
+
+template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0>
 __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   using Tr = GemmTraits<KIND>;
   using acc_t = typename Tr::acc_t;
@@ -116,9 +188,23 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   constexpr int kUnroll = gemm_unroll<MT, WAVES>();
   // Cross-wave partial sums, [wave][tile][reg][lane]: lane-fastest so both the
   // per-register stores and the epilogue's reads (consecutive threads =
-  // consecutive columns = consecutive lanes) are bank-conflict free.
+  // consecutive columns = consecutive lanes) are bank-conflict free.  With the
+  // LayerNorm prologue (PRO = 1) they live in dynamic LDS, over the A image
+  // once the k loop is done.
   using elem_t = typename Tr::elem_t;
-  __shared__ elem_t red[WAVES][MT * NT][4][64];
+  using RedT = elem_t[MT * NT][4][64];
+  extern __shared__ __attribute__((aligned(16))) uint8_t gemm_smem[];
+  RedT* red;
+  if constexpr (PRO == 0) {
+    __shared__ elem_t red_static[WAVES][MT * NT][4][64];
+    red = red_static;
+  } else {
+    red = reinterpret_cast<RedT*>(gemm_smem);
+  }
+  constexpr int ROWS_ = 16 * MT;
+  const int a_stride = ln_row_stride(a.K, Tr::ESIZE);
+  uint8_t* alds = gemm_smem;
+  float* sa_lds = reinterpret_cast<float*>(gemm_smem + (size_t)ROWS_ * a_stride);
 
   const int lane = lane_id();
   const int w = wave_id_uniform();
@@ -173,18 +259,30 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     u32x4 b[kUnroll][NT];
     u32x4 af[kUnroll][MT];
   };
-  auto issue = [&](Batch& bt, int ks) {
+  // do_a / do_b: the LayerNorm-prologue kernel issues a batch's weight loads
+  // before the prologue and its (LDS) A fragments after it
+  auto issue = [&](Batch& bt, int ks, bool do_a = true, bool do_b = true) {
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int kk = ks + u;
       const bool ok = kk < ks1;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
+        if (!do_b) break;
         const uint32_t boff = ok ? b_lane_off[j] + (uint32_t)kk * 1024u : 0xFFFFFFF0u;
         bt.b[u][j] = __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff, 0, 2);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
+        if (!do_a) break;
+        if constexpr (PRO != 0) {
+          // fragment (row mt*16 + (l & 15), group 4 kk + (l >> 4)) of the LDS image
+          const int r = mt * 16 + arow_lane;
+          bt.af[u][mt] = ok ? *reinterpret_cast<const u32x4*>(alds + (size_t)r * a_stride +
+                                                             16 * (4 * kk + kgrp))
+                            : u32x4{0u, 0u, 0u, 0u};
+          continue;
+        }
         const uint32_t koff = (uint32_t)kk * a_kstride + a_kgrp_off;
         const uint32_t aoff = (ok && a_row_off[mt] != 0xFFFFFFF0u) ? a_row_off[mt] + koff : 0xFFFFFFF0u;
         if constexpr ((DIAG & 1) != 0)
@@ -234,7 +332,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     const bool valid = o < ROWS * COLS && m < a.M && n < a.N;
     e_scale[e] = 1.f;
     if constexpr (KIND == GemmKind::I8) {
-      if (valid && a.sa) e_scale[e] *= a.sa[m];
+      if (!PRO && valid && a.sa) e_scale[e] *= a.sa[m];
       if (valid && a.sw) e_scale[e] *= a.sw[n];
     }
     e_bias[e] = valid && a.bias ? a.bias[n] : 0.f;
@@ -243,10 +341,42 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     e_br[e] = kvcol ? (kv.rows ? kv.rows[m] : m) : -1;
   }
 
+  Batch b0, b1;
+  bool b1_pre = false;  // b1's weight loads already issued
+  if constexpr (PRO != 0) {
+    // the first two batches' weights are in flight while the prologue runs
+    if (ks0 < ks1) issue(b0, ks0, false, true);
+    if (ks0 + kUnroll < ks1) {
+      issue(b1, ks0 + kUnroll, false, true);
+      b1_pre = true;
+    }
+    ln_prologue<KIND, ROWS_, WAVES>(a, m0, alds, sa_lds);
+    __syncthreads();
+    if constexpr (KIND == GemmKind::I8) {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {  // the prologue's row scales into the dequant factor
+        const int o = threadIdx.x + e * NTHR;
+        if (o < ROWS * COLS) e_scale[e] *= sa_lds[o / COLS];
+      }
+    }
+    if (a.act_out && blockIdx.x == 0) {  // activation taps: A in packed-A order + scales
+      const int KS = a.KS;
+      for (int i = threadIdx.x; i < ROWS_ * KS * 4; i += NTHR) {
+        const int r = i / (KS * 4), g = i % (KS * 4);
+        const int m = m0 + r;
+        if (m >= a.M) continue;
+        const size_t off = ((size_t)((m >> 4) * KS + (g >> 2)) * 64 + (m & 15) + 16 * (g & 3)) * 16;
+        *reinterpret_cast<u32x4*>(a.act_out + off) =
+            *reinterpret_cast<const u32x4*>(alds + (size_t)r * a_stride + 16 * g);
+      }
+      if (KIND == GemmKind::I8 && a.sa_out && threadIdx.x < ROWS_ && m0 + (int)threadIdx.x < a.M)
+        a.sa_out[m0 + threadIdx.x] = sa_lds[threadIdx.x];
+    }
+  }
+
   {
-    Batch b0, b1;
     int ks = ks0;
-    if (ks < ks1) issue(b0, ks);
+    if (ks < ks1) issue(b0, ks, true, PRO == 0);
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const int o = threadIdx.x + e * NTHR;
@@ -262,7 +392,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       e_page[e] = page;
     }
     while (ks < ks1) {
-      if (ks + kUnroll < ks1) issue(b1, ks + kUnroll);
+      if (ks + kUnroll < ks1) {
+        issue(b1, ks + kUnroll, true, !b1_pre);
+        b1_pre = false;
+      }
       compute(b0);
       ks += kUnroll;
       if (ks >= ks1) break;
@@ -283,6 +416,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     if (stamp && lane == 0) stamp[32 + w] = phase_clock();
     return;
   }
+  if constexpr (PRO != 0) __syncthreads();  // every wave is done with the A image
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -369,10 +503,25 @@ inline int pick_nt(int N, int M) {
   return (ntiles % 2 == 0 && (ntiles / 2) * mblocks >= 192) ? 2 : 1;
 }
 
+// Dynamic LDS of the LayerNorm-prologue kernel: the rows' A image + row
+// scales, or the cross-wave partial sums that reuse it, whichever is larger.
+template <GemmKind KIND, int MT, int NT, int WAVES>
+size_t ln_lds_bytes(int K) {
+  const size_t img = (size_t)16 * MT * ln_row_stride(K, GemmTraits<KIND>::ESIZE) + 16 * MT * 4;
+  const size_t red = (size_t)WAVES * MT * NT * 4 * 64 * 4;
+  return img > red ? img : red;
+}
+constexpr size_t kLnLdsMax = 160 * 1024;
+
 template <GemmKind KIND, int MT, int NT>
 hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t st) {
   const int ntiles = (a.N + 15) / 16;
   const dim3 grid((ntiles + NT - 1) / NT, mblocks);
+  if (a.ln_x) {
+    const size_t lds = ln_lds_bytes<KIND, MT, NT, 8>(a.K);
+    hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1>), grid, dim3(512), lds, st, a);
+    return hipGetLastError();
+  }
   if (waves == 4)
     hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 4>), grid, dim3(256), 0, st, a);
   else
@@ -399,7 +548,7 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t st, int nt_override = 0,
   // (M = 64: o_proj 5.8 -> 4.5 us, mlp_fc2 13.0 -> 9.6 us; the second row
   // block re-reads the weights, mostly from the Infinity Cache)
   int mrows = a.M <= 16 ? 16 : a.M <= 32 ? 32 : 64;
-  if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256) mrows = 32;
+  if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256 && !a.ln_x) mrows = 32;
   if (mrows_override > 0) mrows = mrows_override;
   if (mrows == 16) return launch_gemm_mt<KIND, 1>(a, NT, waves, (a.M + 15) / 16, st);
   if (mrows == 32) return launch_gemm_mt<KIND, 2>(a, NT, waves, (a.M + 31) / 32, st);
@@ -486,8 +635,18 @@ extern "C" int f16_gemm(const void* A, int lda, const void* W_packed, float* C, 
 }
 
 
+bool llm::ln_fusable(int dtype, int M, int K) {
+  const int es = dtype == LLM_I8 ? 1 : 2;
+  if (K % 16 != 0 || (K * es) % 256 != 0 || K > 2048) return false;
+  const int rows = M <= 16 ? 16 : M <= 32 ? 32 : 64;
+  return (size_t)rows * (ln_row_stride(K, es) + 4) <= kLnLdsMax;
+}
+
 int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
-  LLM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0 && g.A && g.W_packed, "weight_gemm: bad arguments");
+  LLM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0 && (g.A || g.ln_x) && g.W_packed,
+              "weight_gemm: bad arguments");
+  LLM_REQUIRE(!g.ln_x || (g.ln_g && g.ln_b && ln_fusable(g.dtype, g.M, g.K)),
+              "weight_gemm: LayerNorm prologue needs gamma / beta and an A image that fits LDS");
   const int kstep = g.dtype == LLM_I8 ? 64 : 32;
   LLM_REQUIRE(g.K % kstep == 0 && g.N % 16 == 0, "weight_gemm: K / N alignment");
   LLM_REQUIRE(g.a_packed || (g.lda >= g.K && g.lda % 16 == 0), "weight_gemm: lda");
@@ -503,6 +662,9 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.c_ld = g.c_ld > 0 ? g.c_ld : g.N;
   LLM_REQUIRE(!g.C16 || g.N % 32 == 0, "weight_gemm: packed fp16 output needs N % 32 == 0");
   a.c16 = static_cast<_Float16*>(g.C16);
+  a.ln_x = g.ln_x; a.ln_g = g.ln_g; a.ln_b = g.ln_b; a.ln_eps = g.ln_eps;
+  a.act_out = static_cast<uint8_t*>(g.act_out);
+  a.sa_out = g.sa_out;
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");

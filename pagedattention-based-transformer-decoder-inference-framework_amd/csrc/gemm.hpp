@@ -41,8 +41,21 @@ struct WeightGemm {
   int c_cols = 0, c_ld = 0;  // 0: N
   void* C16 = nullptr;       // fp16 copy of C in packed-A order with K = N (next GEMM's input)
   const KvAppendView* kv = nullptr;
+  // LayerNorm prologue: A = LN(ln_x) (I8: quantised per row, the row scales
+  // replace sa) computed per workgroup into LDS, when the rows' A image fits
+  // (ln_fusable); act_out / sa_out optionally receive A (packed-A order) and
+  // the row scales (activation taps).  A / sa are then ignored.
+  const float* ln_x = nullptr;
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float ln_eps = 1e-5f;
+  void* act_out = nullptr;
+  float* sa_out = nullptr;
 };
 
 int weight_gemm(const WeightGemm& g, hipStream_t st);
+// Whether weight_gemm can run the LayerNorm prologue for M rows of K (the
+// per-workgroup A image must fit in LDS; K <= 128 groups of 16 bytes).
+bool ln_fusable(int dtype, int M, int K);
 
 }  // namespace llm

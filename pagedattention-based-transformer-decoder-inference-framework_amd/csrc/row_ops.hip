@@ -2,6 +2,7 @@
 // per-row int8 quantisation, embedding gather, KV append into pages, argmax.
 // All are one workgroup per row, vectorised 16 B per lane where the row allows.
 #include "common.hpp"
+#include "ln_wave.hpp"
 #include "row_ops.hpp"
 
 namespace llm {
@@ -162,82 +163,39 @@ __global__ __launch_bounds__(kRowThreads) void quantize_rows_v_kernel(
   if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
 }
 
-template <int VPT>
-__global__ __launch_bounds__(kRowThreads) void layernorm_quant_v_kernel(
-    const float* __restrict__ x, int cols, const float* __restrict__ gamma,
+// LayerNorm (+ int8 quantisation) with one wave per row, 4 rows per
+// workgroup: the shared ln_wave.hpp row routine, so its activations are
+// bit-identical to the weight GEMM's LayerNorm prologue.  q / out16 in
+// packed-A order when pack, else row-major.
+template <int CPL>
+__global__ __launch_bounds__(kRowThreads) void layernorm_wave_kernel(
+    const float* __restrict__ x, int rows, int cols, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
     float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack) {
-  __shared__ float sh[4];
-  const int r = blockIdx.x;
-  const int n4 = cols >> 2;
-  const f32x4* xr = reinterpret_cast<const f32x4*>(x + (size_t)r * cols);
-  const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma);
-  const f32x4* b4 = reinterpret_cast<const f32x4*>(beta);
-  f32x4 v[VPT], gv[VPT], bv[VPT];
+  const int lane = lane_id();
+  const int r = blockIdx.x * (kRowThreads / 64) + wave_id_uniform();
+  if (r >= rows) return;
+  const int K4 = cols >> 2;
+  LnRow<CPL> gm, bt, v;
+  ln_wave_load(gamma, K4, true, gm);
+  ln_wave_load(beta, K4, true, bt);
+  ln_wave_load(x + (size_t)r * cols, K4, true, v);
+  const float am = ln_wave_compute(v, gm, bt, cols, eps);
+  const float scale = 127.f / (am + 1e-6f);
 #pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int c = threadIdx.x + i * kRowThreads;
-    const bool ok = c < n4;
-    v[i] = ok ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-    gv[i] = ok ? g4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-    bv[i] = ok ? b4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < CPL; ++j) {
+    const int c = 64 * j + lane;
+    if (c >= K4) continue;
+    const int k = 4 * c;
+    if (out) reinterpret_cast<f32x4*>(out + (size_t)r * cols)[c] = v.v[j];
+    if (q)
+      *reinterpret_cast<uint32_t*>(q + (pack ? a_frag_off_i8(r, k, cols >> 6) : (size_t)r * cols + k)) =
+          ln_quant4(v.v[j], scale);
+    if (out16)
+      *reinterpret_cast<ln_f16x4*>(out16 + (pack ? a_frag_off_f16(r, k, cols >> 5) : (size_t)r * cols + k)) =
+          ln_half4(v.v[j]);
   }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-  const float mean = block_sum_fast(s, sh) / (float)cols;
-  float vs = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int c = threadIdx.x + i * kRowThreads;
-    if (c < n4) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = v[i][e] - mean;
-        vs = fmaf(d, d, vs);
-      }
-    }
-  }
-  const float var = block_sum_fast(vs, sh) / (float)cols;
-  const float inv_std = (float)(1.0 / (double)sqrtf(var + eps));
-  float am = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float y = __fmul_rn(__fmul_rn(v[i][e] - mean, inv_std), gv[i][e]);
-      v[i][e] = __fadd_rn(y, bv[i][e]);
-      am = fmaxf(am, fabsf(v[i][e]));
-    }
-    const int c = threadIdx.x + i * kRowThreads;
-    if (c < n4) {
-      if (out) reinterpret_cast<f32x4*>(out + (size_t)r * cols)[c] = v[i];
-      if (out16) {
-        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-        const f16x4 h{(_Float16)v[i][0], (_Float16)v[i][1], (_Float16)v[i][2], (_Float16)v[i][3]};
-        if (pack)
-          *reinterpret_cast<f16x4*>(out16 + a_frag_off_f16(r, 4 * c, cols >> 5)) = h;
-        else
-          reinterpret_cast<f16x4*>(out16 + (size_t)r * cols)[c] = h;
-      }
-    }
-  }
-  if (q) {
-    am = block_max_fast(am, sh);  // padding lanes hold beta=0 -> 0, harmless for |max|
-    const float scale = 127.f / (am + 1e-6f);
-    uint32_t* qr = reinterpret_cast<uint32_t*>(q + (size_t)r * cols);
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = threadIdx.x + i * kRowThreads;
-      if (c < n4) {
-        if (pack)
-          *reinterpret_cast<uint32_t*>(q + a_frag_off_i8(r, 4 * c, cols >> 6)) = pack4_i8(v[i], scale);
-        else
-          qr[c] = pack4_i8(v[i], scale);
-      }
-    }
-    if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
-  }
+  if (q && lane == 0) inv_scale[r] = 1.0f / scale;
 }
 
 // VPT (float4 chunks per thread) for a row of `cols`; 0 = use the scalar kernel.
@@ -370,23 +328,25 @@ hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, f
 static hipError_t launch_ln(const float* x, int rows, int cols, const float* g, const float* b,
                             float eps, float* out, int8_t* q, float* inv, _Float16* out16,
                             hipStream_t st, int pack) {
-  const dim3 gr(rows), bl(kRowThreads);
-  const int v = row_vpt(cols);
-  if (pack && (v == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
-  switch (v) {
-#define LN_CASE(V)                                                                              \
-  case V:                                                                                        \
-    hipLaunchKernelGGL(layernorm_quant_v_kernel<V>, gr, bl, 0, st, x, cols, g, b, eps, out, q,   \
-                       inv, out16, pack);                                                        \
-    break;
-    LN_CASE(1) LN_CASE(2) LN_CASE(4) LN_CASE(8) LN_CASE(16)
-#undef LN_CASE
-    default:
-      hipLaunchKernelGGL(layernorm_quant_kernel, gr, bl, (size_t)cols * sizeof(float), st, x, cols,
-                         g, b, eps, out, q, inv, out16);
-      break;
+  const int k4 = cols % 4 == 0 ? cols / 4 : 0;
+  const int cpl = k4 == 0 ? 0 : k4 <= 64 ? 1 : k4 <= 128 ? 2 : k4 <= 256 ? 4 : k4 <= 512 ? 8
+                : k4 <= 1024 ? 16 : k4 <= 2048 ? 32 : 0;
+  if (pack && (cpl == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
+  if (cpl == 0) {  // odd widths (C ABI only): one workgroup per row
+    hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
+                       (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv, out16);
+    return hipGetLastError();
   }
-  return hipGetLastError();
+  const dim3 gr((rows + 3) / 4), bl(kRowThreads);
+#define LN_CASE(C)                                                                              \
+  if (cpl == C) {                                                                               \
+    hipLaunchKernelGGL((layernorm_wave_kernel<C>), gr, bl, 0, st, x, rows, cols, g, b, eps, out, \
+                       q, inv, out16, pack);                                                    \
+    return hipGetLastError();                                                                   \
+  }
+  LN_CASE(1) LN_CASE(2) LN_CASE(4) LN_CASE(8) LN_CASE(16) LN_CASE(32)
+#undef LN_CASE
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,

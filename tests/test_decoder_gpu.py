@@ -536,16 +536,34 @@ def test_prefill_matches_token_by_token(gpu, oracle):
 def test_prefill_decode_kernel_fallback(gpu, oracle):
     """Head dims the MFMA prefill kernel does not take (D = 256) prefill
     through the decode kernel, one row per prompt token (beam_ids = the row,
-    context_lens = p0 + i + 1): only the split order differs from stepping the
-    prompt token by token, so logits agree to 1e-4 and ids exactly."""
-    w = _int8_model(oracle, L=2, H=2, D=256, V=400, S=700, seed=13)
-    V = w["cfg"]["V"]
+    context_lens = p0 + i + 1).  Against stepping the prompt token by token the
+    attention split order and the fp32 order of the GEMM-fused LayerNorm differ
+    (~1e-7): the fp16 CUDADecoder (no int8 rounding to amplify it) agrees to
+    LOGIT_TOL (measured 3e-4 over 530 prompt tokens); the INT8Decoder, where such
+    a difference can flip an int8 activation, to FREE_RUN_TOL."""
+    import llm_decoder
     rng = np.random.default_rng(4)
+    L, H, D, V, S = 2, 2, 256, 400, 700
+    wf = _f16_model(rng, L, H, D, V, S)
+    d = {k: np.ascontiguousarray(v) for k, v in wf.items() if k != "cfg"}
+    for k in ("emb", "wqkv", "wo", "w1", "w2"):
+        d[k] = d[k].view(np.uint16)
+
+    def make_f16(n):
+        dec = llm_decoder.CUDADecoder(L, H, D, H * D, V, S, max_batch=n)
+        dec.set_weights(d)
+        return dec
+
     prompts = [rng.integers(0, V, 530).tolist(), rng.integers(0, V, 9).tolist()]
+    la, lb, nxt = _prefill_vs_stepping(make_f16, prompts, V)
+    for r in range(2):
+        assert rel_err(lb[r], la[r]) < LOGIT_TOL, (r, rel_err(lb[r], la[r]))
+        assert la[r].max() - la[r][nxt[r]] <= LOGIT_TOL * np.abs(la[r]).max()
+    w = _int8_model(oracle, L=2, H=2, D=256, V=400, S=700, seed=13)
     la, lb, nxt = _prefill_vs_stepping(lambda n: _make_gpu_decoder(w, max_batch=n), prompts, V)
     for r in range(2):
-        assert rel_err(lb[r], la[r]) < 1e-4, (r, rel_err(lb[r], la[r]))
-        assert nxt[r] == int(np.argmax(la[r]))
+        assert rel_err(lb[r], la[r]) < FREE_RUN_TOL, (r, rel_err(lb[r], la[r]))
+        assert la[r].max() - la[r][nxt[r]] <= FREE_RUN_TOL * np.abs(la[r]).max()
 
 
 def test_prefill_mfma_fp16_decoder(gpu, oracle):
