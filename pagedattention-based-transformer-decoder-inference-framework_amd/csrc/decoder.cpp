@@ -103,6 +103,11 @@ struct llm_decoder {
   int tap(int l, int stage, const struct Rows& R, int K, hipStream_t st);
   int layer_norm_into(WeightGemm& g, const struct Rows& R, const float* gamma, const float* beta,
                       hipStream_t st);
+  // split-K o_proj / fc2 (I8 decode): int32 partials in `part`, summed with
+  // the GEMM's epilogue by the next LayerNorm launch (pending describes them)
+  DevBuf<int32_t> part;
+  LnPartials pending;
+  bool split_k(const struct Rows& R, int N, int K) const;
 
   ~llm_decoder() {
     if (graph) (void)hipGraphExecDestroy(graph);
@@ -196,12 +201,13 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
     d->attn_ws_bytes = std::max(d->attn_ws_bytes,
                                 pa_decode_workspace_bytes(b, d->H, d->D, d->max_tiles, 0));
   RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
+  RET_IF(d->part.alloc((size_t)4 * B * hid));  // <= 4 k slices of [B][hid]
   d->qa_ld = std::max(hid, inter);
-  // Overlapping the glue of one half of the rows with the other half's
-  // attention (two micro-batches on two streams, ping-pong ordered) was
-  // measured and removed: 3,672 vs 3,621 tok/s free running, 3,156-3,592
-  // ping-pong (the glue slows 4-8x beside a saturating KV scan), and a CU
-  // partition 2,485-2,645.
+  // Splitting the rows into two micro-batches on two streams was measured and
+  // removed: one graph with two branches, two graphs on two
+  // streams, ping-pong attention and a CU partition all lose (C2 -11..-13 %,
+  // C4 -5 %, C3 -0.5..+1 %: the branches do not overlap usefully, and a
+  // saturating KV scan slows the other half's glue 4-8x).
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
   d->h_pos.assign(B, 0);
   *out = d.release();
@@ -372,18 +378,29 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
 // launch writing the packed A the GEMM reads.
 int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamma,
                                  const float* beta, hipStream_t st) {
-  static const int fuse = env_int("LLM_LN_FUSE", 1);  // TEMP A/B knob
-  if (fuse && R.prefill_row < 0 && ln_fusable(wdtype, R.n, hid)) {
+  if (R.prefill_row < 0 && ln_fusable(wdtype, R.n, hid)) {
     g.ln_x = R.x; g.ln_g = gamma; g.ln_b = beta; g.ln_eps = 1e-5f;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
     return LLM_OK;
   }
-  if (wdtype == LLM_I8)
+  if (wdtype == LLM_I8) {
+    // a pending split-K result is summed (and its rows stored to x) first
+    const LnPartials* pp = pending.part ? &pending : nullptr;
     LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, gamma, beta, 1e-5f, nullptr,
-                                       static_cast<int8_t*>(R.act), R.sa, st, 1));
-  else
+                                       static_cast<int8_t*>(R.act), R.sa, st, 1, pp));
+    pending = LnPartials{};
+  } else {
     LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, gamma, beta, 1e-5f, R.act, st, 1));
+  }
   return LLM_OK;
+}
+
+// Split-K for an I8 weight GEMM of N columns whose output feeds a LayerNorm
+// launch (decode rows; not the GEMM-fused LayerNorm): the column grid alone
+// leaves CUs idle, and every workgroup then reads 1/slices of A.
+bool llm_decoder::split_k(const Rows& R, int N, int K) const {
+  return wdtype == LLM_I8 && R.prefill_row < 0 && R.n <= 64 && !ln_fusable(wdtype, R.n, hid) &&
+         gemm_kslices(N, R.n, K / 64) > 1;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
@@ -434,7 +451,12 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   if (i8) RET_IF(tap(l, 1, R, hid, st));
   g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = R.x;
   if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
+  if (split_k(R, hid, hid)) {  // partials -> LN2 (x rebuilt there)
+    g.partial = 1; g.acc_out = part.p; g.C = nullptr;
+    pending = LnPartials{part.p, gemm_kslices(hid, R.n, hid / 64), R.sa, g.sw, nullptr, R.x};
+  }
   RET_IF(weight_gemm(g, st));
+  g.partial = 0; g.acc_out = nullptr;
   // LN2 -> mlp_fc1 (+b1, ReLU)
   RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
@@ -461,6 +483,10 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
+  if (l + 1 < L && split_k(R, hid, inter)) {  // partials -> the next layer's LN1
+    g.partial = 1; g.acc_out = part.p; g.C = nullptr; g.bias = nullptr;
+    pending = LnPartials{part.p, gemm_kslices(hid, R.n, inter / 64), R.sa, g.sw, b2.p + lh, R.x};
+  }
   return weight_gemm(g, st);
 }
 

@@ -68,6 +68,10 @@ struct GemmArgs {
   float ln_eps;
   uint8_t* act_out;       // optional: workgroups with blockIdx.x == 0 store A (packed-A order)
   float* sa_out;          //   and the I8 row scales (activation taps)
+  // split-K (I8, gridDim.z = k slices): slice z sums k-steps [z KS/Z, (z+1) KS/Z)
+  // and stores its exact int32 partial sums to acc_out + z * M * N ([M][N]),
+  // nothing else; the consumer adds the slices and applies the epilogue.
+  int partial;
 };
 
 // LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
@@ -217,8 +221,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   // workgroups of an XCD read different A fragments (all of them read all of
   // A), instead of every workgroup hitting the same L2 lines.
   const int wr = (w + blockIdx.x) % WAVES;
-  const int ks0 = (wr * a.KS) / WAVES;
-  const int ks1 = ((wr + 1) * a.KS) / WAVES;
+  const int kz0 = (int)((blockIdx.z * a.KS) / gridDim.z);  // this k slice (split-K)
+  const int kzn = (int)(((blockIdx.z + 1) * a.KS) / gridDim.z) - kz0;
+  const int ks0 = kz0 + (wr * kzn) / WAVES;
+  const int ks1 = kz0 + ((wr + 1) * kzn) / WAVES;
   const int ntiles = (a.N + 15) >> 4;
 
   // A descriptor: rows >= M (and anything past the matrix) read as zero.
@@ -446,6 +452,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       int32_t s = 0;
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][reg][src_lane];
+      if (a.partial) {
+        a.acc_out[((size_t)blockIdx.z * a.M + m) * a.N + n] = s;
+        continue;
+      }
       if (a.acc_out) a.acc_out[(size_t)m * a.N + n] = s;
       y = (float)s * e_scale[e];
       if (a.bias) y = y + e_bias[e];
@@ -514,9 +524,9 @@ size_t ln_lds_bytes(int K) {
 constexpr size_t kLnLdsMax = 160 * 1024;
 
 template <GemmKind KIND, int MT, int NT>
-hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t st) {
+hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t st, int kslices) {
   const int ntiles = (a.N + 15) / 16;
-  const dim3 grid((ntiles + NT - 1) / NT, mblocks);
+  const dim3 grid((ntiles + NT - 1) / NT, mblocks, kslices);
   if (a.ln_x) {
     const size_t lds = ln_lds_bytes<KIND, MT, NT, 8>(a.K);
     hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1>), grid, dim3(512), lds, st, a);
@@ -530,10 +540,24 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t
 }
 
 template <GemmKind KIND, int MT>
-hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hipStream_t st) {
-  return NT == 2 ? launch_gemm_nt<KIND, MT, 2>(a, waves, mblocks, st)
-                 : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st);
+hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hipStream_t st,
+                          int kslices) {
+  return NT == 2 ? launch_gemm_nt<KIND, MT, 2>(a, waves, mblocks, st, kslices)
+                 : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st, kslices);
 }
+
+}  // namespace
+
+// k slices of a split-K launch: enough to give 256 workgroups (the CU count)
+// at one column tile per workgroup, at most 4, each slice >= 8 k-steps.
+int gemm_kslices(int N, int M, int KS) {
+  const int groups = ((N + 15) / 16) * ((M + 63) / 64);
+  int ks = 1;
+  while (ks < 4 && groups * ks < 256 && KS / (2 * ks) >= 8) ks *= 2;
+  return ks;
+}
+
+namespace {
 
 // Waves per workgroup (they split K): 8.  The 4-wave form (twice the
 // k-steps per wave) is kept for the tuning entry.
@@ -548,11 +572,15 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t st, int nt_override = 0,
   // (M = 64: o_proj 5.8 -> 4.5 us, mlp_fc2 13.0 -> 9.6 us; the second row
   // block re-reads the weights, mostly from the Infinity Cache)
   int mrows = a.M <= 16 ? 16 : a.M <= 32 ? 32 : 64;
-  if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256 && !a.ln_x) mrows = 32;
+  // no split-K: 32 rows per workgroup when the column grid alone cannot fill
+  // the CUs (the second row block re-reads the weights, mostly from the
+  // Infinity Cache); split-K fills them with k slices instead
+  if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256 && !a.ln_x && !a.partial) mrows = 32;
   if (mrows_override > 0) mrows = mrows_override;
-  if (mrows == 16) return launch_gemm_mt<KIND, 1>(a, NT, waves, (a.M + 15) / 16, st);
-  if (mrows == 32) return launch_gemm_mt<KIND, 2>(a, NT, waves, (a.M + 31) / 32, st);
-  return launch_gemm_mt<KIND, 4>(a, NT, waves, (a.M + 63) / 64, st);
+  const int ks = a.partial ? gemm_kslices(a.N, a.M, a.KS) : 1;
+  if (mrows == 16) return launch_gemm_mt<KIND, 1>(a, NT, waves, (a.M + 15) / 16, st, ks);
+  if (mrows == 32) return launch_gemm_mt<KIND, 2>(a, NT, waves, (a.M + 31) / 32, st, ks);
+  return launch_gemm_mt<KIND, 4>(a, NT, waves, (a.M + 63) / 64, st, ks);
 }
 
 }  // namespace
@@ -635,10 +663,17 @@ extern "C" int f16_gemm(const void* A, int lda, const void* W_packed, float* C, 
 }
 
 
+// The prologue pays off only while the fp32 rows every workgroup reads stay
+// small: all workgroups read all of them, and a CU takes in L2-resident data
+// at only ~80-120 GB/s (scripts/micro/bcast_read.hip: 256 KB per workgroup
+// +2.2 us, 512 KB +6.4 us).  Same-box A/B of the decode step
+// (scripts/gpu_ab.sh): C2 (16 rows x 768, 48 KB) +1.5-5 %; C4 (32 x 2048,
+// 256 KB) -7 %; C3 (64 x 2048, 512 KB) -4 %.  So: at most 64 KB of rows.
 bool llm::ln_fusable(int dtype, int M, int K) {
   const int es = dtype == LLM_I8 ? 1 : 2;
   if (K % 16 != 0 || (K * es) % 256 != 0 || K > 2048) return false;
   const int rows = M <= 16 ? 16 : M <= 32 ? 32 : 64;
+  if ((size_t)rows * K * sizeof(float) > 64 * 1024) return false;
   return (size_t)rows * (ln_row_stride(K, es) + 4) <= kLnLdsMax;
 }
 
@@ -665,6 +700,12 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.ln_x = g.ln_x; a.ln_g = g.ln_g; a.ln_b = g.ln_b; a.ln_eps = g.ln_eps;
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;
+  if (g.partial) {
+    LLM_REQUIRE(g.dtype == LLM_I8 && g.acc_out && !g.ln_x && !g.kv && !g.C16,
+                "weight_gemm: split-K is an I8 GEMM writing only int32 partials");
+    a.partial = 1;
+    a.acc_out = g.acc_out;
+  }
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");

@@ -51,11 +51,29 @@ struct WeightGemm {
   float ln_eps = 1e-5f;
   void* act_out = nullptr;
   float* sa_out = nullptr;
+  // split-K (I8): k slices (gemm_kslices) write exact int32 partial sums to
+  // acc_out [slices][M][N] and nothing else; the consumer (a LayerNorm launch
+  // reading LnPartials) sums them and applies the epilogue
+  int partial = 0;
+  int32_t* acc_out = nullptr;
+};
+
+// Split-K input of a LayerNorm launch: x[m][n] = (float)(sum_z part[z][m][n])
+// * (sa[m] * sw[n]) + bias[n] -- bit for bit the GEMM epilogue it replaces.
+struct LnPartials {
+  const int32_t* part = nullptr;
+  int slices = 0;
+  const float* sa = nullptr;
+  const float* sw = nullptr;
+  const float* bias = nullptr;  // may be NULL
+  float* x_out = nullptr;       // the reconstructed rows (fp32 [M][N])
 };
 
 int weight_gemm(const WeightGemm& g, hipStream_t st);
 // Whether weight_gemm can run the LayerNorm prologue for M rows of K (the
 // per-workgroup A image must fit in LDS; K <= 128 groups of 16 bytes).
 bool ln_fusable(int dtype, int M, int K);
+// k slices weight_gemm uses for a split-K launch of N columns, M rows, KS k-steps
+int gemm_kslices(int N, int M, int KS);
 
 }  // namespace llm

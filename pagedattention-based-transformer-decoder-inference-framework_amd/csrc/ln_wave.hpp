@@ -1,8 +1,7 @@
-// One-wave-per-row LayerNorm (+ int8 quantisation) shared by the LayerNorm
-// launch (row_ops.hip layernorm_wave_kernel) and the weight GEMM's LayerNorm
-// prologue (gemm.hip), so both produce bit-identical activations: a prompt
-// prefilled through the launch and the same tokens stepped through the fused
-// GEMM see the same int8 / fp16 inputs.
+// One-wave-per-row LayerNorm (+ int8 quantisation) of the weight GEMM's
+// LayerNorm prologue (gemm.hip), plus the quantise / fp16 helpers the
+// LayerNorm launch (row_ops.hip layernorm_rows_kernel, 256 threads per row)
+// shares with it.
 //
 // LayerNorm<T>::forward (decoder/layer_norm.hpp:20-37): biased variance,
 // inv_std = 1.0 / sqrt(var + eps) (double division of the float sqrt), y =

@@ -2,6 +2,7 @@
 // per-row int8 quantisation, embedding gather, KV append into pages, argmax.
 // All are one workgroup per row, vectorised 16 B per lane where the row allows.
 #include "common.hpp"
+#include "gemm.hpp"
 #include "ln_wave.hpp"
 #include "row_ops.hpp"
 
@@ -163,39 +164,113 @@ __global__ __launch_bounds__(kRowThreads) void quantize_rows_v_kernel(
   if (threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
 }
 
-// LayerNorm (+ int8 quantisation) with one wave per row, 4 rows per
-// workgroup: the shared ln_wave.hpp row routine, so its activations are
-// bit-identical to the weight GEMM's LayerNorm prologue.  q / out16 in
-// packed-A order when pack, else row-major.
-template <int CPL>
-__global__ __launch_bounds__(kRowThreads) void layernorm_wave_kernel(
+// LayerNorm (+ int8 quantisation) launch, one 256-thread workgroup per row:
+// every thread loads its VPT float4 chunks (chunk c = threadIdx.x + 256 v) --
+// of x, or of a split-K GEMM's int32 partial slices plus that GEMM's scales
+// and bias (pp.part, LnPartials: the row is rebuilt with the GEMM's epilogue
+// and stored to pp.x_out) -- and gamma / beta, all in ONE memory round trip;
+// wave DPP sums + one LDS exchange per reduction.  Numerics of
+// LayerNorm<T>::forward (decoder/layer_norm.hpp:20-37) and int8_quant.cpp as
+// ln_wave.hpp (the GEMM prologue); only the fp32 summation order differs.
+// q / out16 in packed-A order when pack.
+template <int VPT>
+__global__ __launch_bounds__(kRowThreads) void layernorm_rows_kernel(
     const float* __restrict__ x, int rows, int cols, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
-    float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack) {
-  const int lane = lane_id();
-  const int r = blockIdx.x * (kRowThreads / 64) + wave_id_uniform();
-  if (r >= rows) return;
-  const int K4 = cols >> 2;
-  LnRow<CPL> gm, bt, v;
-  ln_wave_load(gamma, K4, true, gm);
-  ln_wave_load(beta, K4, true, bt);
-  ln_wave_load(x + (size_t)r * cols, K4, true, v);
-  const float am = ln_wave_compute(v, gm, bt, cols, eps);
-  const float scale = 127.f / (am + 1e-6f);
+    float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack, LnPartials pp) {
+  __shared__ float sh[4];
+  const int r = blockIdx.x;
+  const int n4 = cols >> 2;
+  const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma);
+  const f32x4* b4 = reinterpret_cast<const f32x4*>(beta);
+  f32x4 v[VPT], gv[VPT], bv[VPT];
+  bool from_partials = false;
+  if constexpr (VPT <= 4) from_partials = pp.part != nullptr;  // (launch_ln checks)
+  if (from_partials) {
+    constexpr int kMaxSlices = 4;
+    i32x4 pv[kMaxSlices][VPT];
+    f32x4 sw[VPT], bi[VPT];
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = 64 * j + lane;
-    if (c >= K4) continue;
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kRowThreads;
+      const bool ok = c < n4;
+#pragma unroll
+      for (int z = 0; z < kMaxSlices; ++z)
+        pv[z][i] = ok && z < pp.slices
+                       ? reinterpret_cast<const i32x4*>(pp.part + ((size_t)z * rows + r) * cols)[c]
+                       : i32x4{0, 0, 0, 0};
+      sw[i] = ok ? reinterpret_cast<const f32x4*>(pp.sw)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      bi[i] = ok && pp.bias ? reinterpret_cast<const f32x4*>(pp.bias)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      gv[i] = ok ? g4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      bv[i] = ok ? b4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const float sa = pp.sa[r];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const i32x4 acc = (pv[0][i] + pv[1][i]) + (pv[2][i] + pv[3][i]);  // exact
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // the GEMM epilogue: acc * (sa * sw), then + bias
+        float y = __fmul_rn((float)acc[e], __fmul_rn(sa, sw[i][e]));
+        if (pp.bias) y = __fadd_rn(y, bi[i][e]);
+        v[i][e] = y;
+      }
+      const int c = threadIdx.x + i * kRowThreads;
+      if (pp.x_out && c < n4) reinterpret_cast<f32x4*>(pp.x_out + (size_t)r * cols)[c] = v[i];
+    }
+  } else {
+    const f32x4* xr = reinterpret_cast<const f32x4*>(x + (size_t)r * cols);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kRowThreads;
+      const bool ok = c < n4;
+      v[i] = ok ? xr[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      gv[i] = ok ? g4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      bv[i] = ok ? b4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  const float mean = block_sum_fast(s, sh) / (float)cols;
+  float vs = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kRowThreads;
+    if (c < n4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[i][e] - mean;
+        vs = fmaf(d, d, vs);
+      }
+    }
+  }
+  const float var = block_sum_fast(vs, sh) / (float)cols;
+  const float inv_std = (float)(1.0 / (double)sqrtf(var + eps));
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float y = __fmul_rn(__fmul_rn(v[i][e] - mean, inv_std), gv[i][e]);
+      v[i][e] = __fadd_rn(y, bv[i][e]);
+      am = fmaxf(am, fabsf(v[i][e]));  // padding chunks: beta 0 -> 0
+    }
+  }
+  const float scale = q ? 127.f / (block_max_fast(am, sh) + 1e-6f) : 1.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * kRowThreads;
+    if (c >= n4) continue;
     const int k = 4 * c;
-    if (out) reinterpret_cast<f32x4*>(out + (size_t)r * cols)[c] = v.v[j];
+    if (out) reinterpret_cast<f32x4*>(out + (size_t)r * cols)[c] = v[i];
     if (q)
       *reinterpret_cast<uint32_t*>(q + (pack ? a_frag_off_i8(r, k, cols >> 6) : (size_t)r * cols + k)) =
-          ln_quant4(v.v[j], scale);
+          ln_quant4(v[i], scale);
     if (out16)
       *reinterpret_cast<ln_f16x4*>(out16 + (pack ? a_frag_off_f16(r, k, cols >> 5) : (size_t)r * cols + k)) =
-          ln_half4(v.v[j]);
+          ln_half4(v[i]);
   }
-  if (q && lane == 0) inv_scale[r] = 1.0f / scale;
+  if (q && threadIdx.x == 0) inv_scale[r] = 1.0f / scale;
 }
 
 // VPT (float4 chunks per thread) for a row of `cols`; 0 = use the scalar kernel.
@@ -327,32 +402,32 @@ hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, f
 
 static hipError_t launch_ln(const float* x, int rows, int cols, const float* g, const float* b,
                             float eps, float* out, int8_t* q, float* inv, _Float16* out16,
-                            hipStream_t st, int pack) {
-  const int k4 = cols % 4 == 0 ? cols / 4 : 0;
-  const int cpl = k4 == 0 ? 0 : k4 <= 64 ? 1 : k4 <= 128 ? 2 : k4 <= 256 ? 4 : k4 <= 512 ? 8
-                : k4 <= 1024 ? 16 : k4 <= 2048 ? 32 : 0;
-  if (pack && (cpl == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
-  if (cpl == 0) {  // odd widths (C ABI only): one workgroup per row
+                            hipStream_t st, int pack, const LnPartials* pp = nullptr) {
+  const LnPartials none{};
+  const int v = row_vpt(cols);
+  if (pp && pp->part && (v == 0 || v > 4 || pp->slices > 4)) return hipErrorInvalidValue;
+  if (pack && (v == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
+  if (v == 0) {  // odd widths (C ABI only)
     hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
                        (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv, out16);
     return hipGetLastError();
   }
-  const dim3 gr((rows + 3) / 4), bl(kRowThreads);
-#define LN_CASE(C)                                                                              \
-  if (cpl == C) {                                                                               \
-    hipLaunchKernelGGL((layernorm_wave_kernel<C>), gr, bl, 0, st, x, rows, cols, g, b, eps, out, \
-                       q, inv, out16, pack);                                                    \
+  const dim3 gr(rows), bl(kRowThreads);
+#define LN_CASE(V)                                                                              \
+  if (v == V) {                                                                                 \
+    hipLaunchKernelGGL((layernorm_rows_kernel<V>), gr, bl, 0, st, x, rows, cols, g, b, eps, out, \
+                       q, inv, out16, pack, pp ? *pp : none);                                   \
     return hipGetLastError();                                                                   \
   }
-  LN_CASE(1) LN_CASE(2) LN_CASE(4) LN_CASE(8) LN_CASE(16) LN_CASE(32)
+  LN_CASE(1) LN_CASE(2) LN_CASE(4) LN_CASE(8) LN_CASE(16)
 #undef LN_CASE
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
-                                  hipStream_t st, int pack) {
-  return launch_ln(x, rows, cols, g, b, eps, out, q, inv, nullptr, st, pack);
+                                  hipStream_t st, int pack, const LnPartials* pp) {
+  return launch_ln(x, rows, cols, g, b, eps, out, q, inv, nullptr, st, pack, pp);
 }
 
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,

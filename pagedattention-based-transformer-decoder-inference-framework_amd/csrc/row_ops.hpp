@@ -12,9 +12,11 @@ namespace llm {
 // needs cols % 64 == 0), consumed by the weight GEMMs with a_packed.
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv,
                                 hipStream_t st, int pack = 0);
+struct LnPartials;
+// pp (optional): rebuild x from a split-K GEMM's int32 partials first (gemm.hpp)
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
-                                  hipStream_t st, int pack = 0);
+                                  hipStream_t st, int pack = 0, const LnPartials* pp = nullptr);
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
                                 const float* b, float eps, void* out16, hipStream_t st,
                                 int pack = 0);
