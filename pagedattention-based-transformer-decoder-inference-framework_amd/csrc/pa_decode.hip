@@ -37,6 +37,7 @@
 //   * scores are kept in log2 units (q pre-scaled by sm_scale*log2(e)) so
 //     every exponential is one v_exp_f32.
 #include "common.hpp"
+#include "ln_wave.hpp"
 #include "pa_decode.hpp"
 #include "row_ops.hpp"
 
@@ -620,7 +621,7 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
         // unconditional loads (clamped in range) so all issue before the first wait
         v[s2][j] = pa[(size_t)min(s2, max(ns - 1, 0)) * a.D + min(d, a.D - 1)];
       }
-    const float M = wave_max(fmaxf(m0, m1));
+    const float M = ln_wave_max(fmaxf(m0, m1));
     float* dst = row + h * a.D;
     if (ns <= 0 || M <= 0.5f * kNegSentinel) {
       for (int d = lane; d < a.D; d += 64) dst[d] = 0.f;
@@ -628,9 +629,18 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
     }
     const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
     const float w1 = 64 + lane < ns ? __builtin_amdgcn_exp2f(m1 - M) : 0.f;
-    // same summation order as pa_merge_kernel: s = 0, 1, ... (sequential)
+    // same summation order as pa_merge_kernel: s = 0, 1, ... (sequential);
+    // split s's (l, w) come from lane s by readlane (SALU broadcast, no LDS
+    // round trip per split), the first kMergeBatch unrolled
     float L = 0.f;
-    for (int s2 = 0; s2 < ns; ++s2) {
+#pragma unroll
+    for (int s2 = 0; s2 < kMergeBatch; ++s2)
+      if (s2 < ns) {
+        const float ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l0), s2));
+        const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
+        L += ls * ws;
+      }
+    for (int s2 = kMergeBatch; s2 < ns; ++s2) {
       const float ls = s2 < 64 ? __shfl(l0, s2, 64) : __shfl(l1, s2 - 64, 64);
       const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
       L += ls * ws;
@@ -641,7 +651,7 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
     for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
 #pragma unroll
     for (int s2 = 0; s2 < kMergeBatch; ++s2) {
-      const float ws = __shfl(w0, s2, 64);  // 0 for s2 >= ns
+      const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));  // 0 past ns
 #pragma unroll
       for (int j = 0; j < DPL; ++j) acc[j] += v[s2][j] * ws;
     }
@@ -678,7 +688,7 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
       a.out16[a.pack ? a_frag_off_f16(b, i, hid >> 5) : (size_t)b * hid + i] = (_Float16)v;
   }
   if (!a.q) return;
-  am = wave_max(am);
+  am = ln_wave_max(am);  // DPP (wave_max shuffles through LDS)
   if (lane == 0) sh[w] = am;
   __syncthreads();
   am = sh[0];
