@@ -187,6 +187,18 @@ int i8_gemm(const int8_t* A, int lda, const void* W_packed, int32_t* acc_out, fl
             int M, int N, int K, const float* sa, const float* sw, const float* bias,
             int act, void* stream);
 
+/* Batched INT8 matmul with int8 output, the full form of dnnl_matmul_int8
+ * (attention_cpu/dnnl_matmul_int8.cpp:7-75, dnnl_matmul_int8.hpp:5-13):
+ *   A s8 [batch][M][K], B s8 [batch][K][N] (row-major, unpacked), C s8 [batch][M][N]
+ *   y = act((float(acc) + bias[n]) * alpha),  alpha = scale_a * scale_b / scale_c
+ *   C = round_half_even(saturate(y, -128, 127))
+ * bias (fp32 [N]) may be NULL; act LLM_ACT_NONE / RELU / GELU (erf).  Any M, N,
+ * K (K < 131072); batch * M * N == 0 is a no-op.  The reference returns false
+ * on any failure; this returns a status code (llm_last_error()). */
+int i8_matmul_s8(const int8_t* A, const int8_t* B, int8_t* C, int batch, int M, int N, int K,
+                 float scale_a, float scale_b, float scale_c, const float* bias, int act,
+                 void* stream);
+
 /* FP16 GEMM with fp32 accumulate (CUDADecoder weights):
  *   C[m,n] = act(sum_k A[m,k] W[k,n] + bias[n]),  A fp16 [M][K], K % 32 == 0. */
 int f16_gemm(const void* A, int lda, const void* W_packed, float* C, int M, int N, int K,

@@ -311,6 +311,38 @@ def unpack_a_i8(packed: np.ndarray, rows: int, K: int) -> np.ndarray:
     return np.asarray(packed).reshape(-1)[off]
 
 
+def dnnl_matmul_int8_np(A, B, scaleA, scaleB, scaleC=1.0, bias=None, activation=""):
+    """Restatement of dnnl_matmul_int8 (attention_cpu/dnnl_matmul_int8.cpp:7-75):
+    A s8 [BATCH][M][K] x B s8 [BATCH][K][N] -> C s8 [BATCH][M][N] with
+    alpha = scaleA * scaleB / scaleC (:40) as the output scale, an optional f32
+    bias [N] (:23, 34-37) and a relu / gelu_erf post-op (:43-50).  oneDNN is not
+    in this image, so the order is oneDNN v2's reference matmul, restated:
+    res = float(acc) (+ bias); res *= alpha; post-op; saturate to [-128, 127];
+    round half to even (parity unpinned against oneDNN itself).  Every step is
+    float32-rounded; gelu's erf is evaluated in float64 and rounded, so it can
+    differ from a float32 erff by an ulp: returns (C, y) with y the value before
+    rounding, for tests to skip ties at .5 boundaries."""
+    A = np.asarray(A, np.int8)
+    B = np.asarray(B, np.int8)
+    acc = np.matmul(A.astype(np.int64), B.astype(np.int64))
+    assert np.abs(acc).max(initial=0) < 2 ** 31
+    f = np.float32
+    alpha = f(f(f(scaleA) * f(scaleB)) / f(scaleC))
+    y = acc.astype(np.int32).astype(f)
+    if bias is not None:
+        y = (y + np.asarray(bias, f)[None, None, :]).astype(f)
+    y = (y * alpha).astype(f)
+    if activation == "relu":
+        y = np.maximum(y, f(0))
+    elif activation == "gelu":
+        import math
+        t = (y * f(0.70710678118654752)).astype(f)
+        erf = np.vectorize(math.erf, otypes=[np.float64])(t.astype(np.float64)).astype(f)
+        y = ((f(0.5) * y).astype(f) * (f(1) + erf).astype(f)).astype(f)
+    y = np.clip(y, f(-128), f(127))
+    return np.rint(y).astype(np.int8), y
+
+
 def quantize_rows_np(x: np.ndarray):
     """numpy mirror of int8_quant.cpp per-row quantisation (round half away)."""
     x = np.asarray(x, np.float32)

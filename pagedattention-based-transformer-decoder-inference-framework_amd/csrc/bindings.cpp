@@ -519,6 +519,24 @@ PYBIND11_MODULE(llm_decoder, m) {
         py::arg("workspace_bytes") = 0, py::arg("stream") = 0, py::arg("row_group") = 1,
         py::arg("eos_token") = -1, py::arg("eos_threshold") = 0.0f, py::arg("probs_out") = 0,
         py::arg("scores_out") = 0);
+  m.def("dnnl_matmul_int8",
+        [](uintptr_t A, uintptr_t B, uintptr_t C, int BATCH, int M, int N, int K, float scaleA,
+           float scaleB, float scaleC, uintptr_t bias, const std::string& activation,
+           uintptr_t stream) {
+          // dnnl_matmul_int8 (attention_cpu/dnnl_matmul_int8.hpp:5-13): device
+          // pointers; false on any failure, as the reference's catch (...) (:73-74);
+          // an unknown activation adds no post-op (:44-50)
+          const int act = activation == "relu" ? LLM_ACT_RELU
+                          : activation == "gelu" ? LLM_ACT_GELU : LLM_ACT_NONE;
+          py::gil_scoped_release nogil;
+          return i8_matmul_s8(reinterpret_cast<const int8_t*>(A), reinterpret_cast<const int8_t*>(B),
+                              reinterpret_cast<int8_t*>(C), BATCH, M, N, K, scaleA, scaleB, scaleC,
+                              reinterpret_cast<const float*>(bias), act,
+                              reinterpret_cast<void*>(stream)) == LLM_OK;
+        },
+        py::arg("A"), py::arg("B"), py::arg("C"), py::arg("BATCH"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("scaleA"), py::arg("scaleB"), py::arg("scaleC") = 1.0f,
+        py::arg("bias") = 0, py::arg("activation") = "", py::arg("stream") = 0);
   m.def("workspace_bytes", &pa_decode_workspace_bytes, py::arg("B"), py::arg("H"), py::arg("D"),
         py::arg("max_tiles"), py::arg("pages_per_split") = 0);
 }

@@ -71,6 +71,8 @@ _SIGS = {
     "gemm_pack_weights": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "i8_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                         c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "i8_matmul_s8": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float,
+                             c_float, c_float, c_void_p, c_int, c_void_p]),
     "f16_gemm": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                          c_int, c_void_p]),
     "lm_head": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
@@ -308,6 +310,28 @@ def i8_gemm(A, W_packed, N, *, sa=None, sw=None, bias=None, act=0, want_acc=True
     check(lib.i8_gemm(ptr(A), A.stride(0), ptr(W_packed), ptr(acc), ptr(C), M, N, K, ptr(sa),
                       ptr(sw), ptr(bias), act, stream_ptr(stream)))
     return acc, C
+
+
+_ACT_NAMES = {"": LLM_ACT_NONE, "relu": LLM_ACT_RELU, "gelu": LLM_ACT_GELU}
+
+
+def dnnl_matmul_int8(A, B, C, BATCH, M, N, K, scaleA, scaleB, scaleC=1.0, bias=None,
+                     activation="", stream=None) -> bool:
+    """dnnl_matmul_int8 (attention_cpu/dnnl_matmul_int8.hpp:5-13) over device tensors:
+    A int8 [BATCH][M][K], B int8 [BATCH][K][N], C int8 [BATCH][M][N] (written),
+    bias fp32 [N] or None, activation "" / "relu" / "gelu".  Like the reference it
+    returns False on any failure (and an unknown activation string is ignored, as
+    the reference's post-op chain ignores it, dnnl_matmul_int8.cpp:44-50)."""
+    import torch
+    lib = load()
+    act = _ACT_NAMES.get(activation, LLM_ACT_NONE)
+    for t, n in ((A, BATCH * M * K), (B, BATCH * K * N), (C, BATCH * M * N)):
+        if t.dtype != torch.int8 or not t.is_contiguous() or t.numel() < n:
+            return False
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() < N):
+        return False
+    return lib.i8_matmul_s8(ptr(A), ptr(B), ptr(C), BATCH, M, N, K, scaleA, scaleB, scaleC,
+                            ptr(bias), act, stream_ptr(stream)) == LLM_OK
 
 
 def f16_gemm(A, W_packed, N, *, bias=None, act=0, stream=None):

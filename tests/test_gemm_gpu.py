@@ -201,3 +201,59 @@ def test_sample_rows_distribution(gpu):
     assert np.all(np.abs(cnt - n * pr) < 5 * sigma + 1), (cnt, n * pr)
     tk = torch.stack([llm_capi.sample_rows(d, T, 3, 1.0, seed=9, counter=c) for c in range(300)])
     assert set(tk.cpu().numpy().ravel().tolist()) <= {0, 6, 1}
+
+
+@pytest.mark.parametrize("batch,M,N,K", [
+    (1, 1, 1, 1), (1, 64, 64, 64), (3, 17, 33, 70), (2, 130, 70, 200), (1, 5, 1000, 2048),
+    (4, 64, 256, 4096),
+])
+@pytest.mark.parametrize("activation", ["", "relu", "gelu"])
+def test_dnnl_matmul_int8_s8_batch(gpu, batch, M, N, K, activation):
+    """i8_matmul_s8 (the s8-output, BATCH form of dnnl_matmul_int8,
+    attention_cpu/dnnl_matmul_int8.cpp:7-75) vs the oracle restatement: exact
+    int8 outputs; for gelu only values within 1e-3 of a .5 rounding boundary may
+    differ, by one (erff vs the oracle's rounded float64 erf)."""
+    import torch
+    import llm_capi
+    from oracle.oracle import dnnl_matmul_int8_np
+    rng = np.random.default_rng(batch * 1000 + M + N + K)
+    A = rng.integers(-128, 128, (batch, M, K), dtype=np.int8)
+    B = rng.integers(-128, 128, (batch, K, N), dtype=np.int8)
+    bias = (rng.standard_normal(N) * 500).astype(np.float32)
+    # output scale sized so the results straddle the int8 range
+    sA, sB = 0.02, 0.05
+    sC = float(sA * sB * 128 * 128 * np.sqrt(K) / 180)
+    for b in (None, bias):
+        want, y = dnnl_matmul_int8_np(A, B, sA, sB, sC, b, activation)
+        C = torch.zeros((batch, M, N), dtype=torch.int8, device="cuda")
+        ok = llm_capi.dnnl_matmul_int8(_dev(A), _dev(B), C, batch, M, N, K, sA, sB, sC,
+                                       None if b is None else _dev(b), activation)
+        assert ok
+        got = C.cpu().numpy()
+        if activation == "gelu":
+            tie = np.abs(np.abs(y - np.trunc(y)) - 0.5) < 1e-3
+            assert np.all(np.abs(got.astype(int) - want.astype(int)) <= tie.astype(int))
+        else:
+            np.testing.assert_array_equal(got, want)
+        assert (got == 127).any() or (got == -128).any() or M * N < 64  # saturation exercised
+
+
+def test_dnnl_matmul_int8_refusals(gpu):
+    """False on a bad call, as the reference's catch (...) (dnnl_matmul_int8.cpp:73-74),
+    through both the ctypes mirror and the pybind module; C untouched."""
+    import torch
+    import llm_capi
+    import llm_decoder
+    A = torch.ones((1, 4, 8), dtype=torch.int8, device="cuda")
+    B = torch.ones((1, 8, 4), dtype=torch.int8, device="cuda")
+    C = torch.full((1, 4, 4), 7, dtype=torch.int8, device="cuda")
+    assert not llm_capi.dnnl_matmul_int8(A, B, C, 1, 4, 4, 8, 1.0, 1.0, 0.0)  # scaleC 0
+    assert not llm_capi.dnnl_matmul_int8(A, B, C, 1, 4, 4, 200000, 1.0, 1.0)  # K too large
+    assert not llm_capi.dnnl_matmul_int8(A.float(), B, C, 1, 4, 4, 8, 1.0, 1.0)
+    assert (C == 7).all()
+    assert llm_decoder.dnnl_matmul_int8(A.data_ptr(), B.data_ptr(), C.data_ptr(), 1, 4, 4, 8,
+                                        1.0, 1.0, 2.0, 0, "relu")
+    torch.cuda.synchronize()
+    assert (C == 4).all()  # 8 / 2
+    assert not llm_decoder.dnnl_matmul_int8(A.data_ptr(), B.data_ptr(), C.data_ptr(), 1, 4, 4, 8,
+                                            1.0, 1.0, 0.0)

@@ -135,6 +135,29 @@ def test_oracle_i8_gemm_epilogue(oracle):
     np.testing.assert_allclose(C2, g, rtol=1e-5, atol=1e-5)
 
 
+def test_oracle_dnnl_matmul_int8_known_answers():
+    """dnnl_matmul_int8 restatement (s8 output, BATCH): hand-computed values for
+    the bias-then-scale order, round half to even, saturation and the post-ops;
+    batches are independent.  Parity unpinned against oneDNN (absent here)."""
+    from oracle.oracle import dnnl_matmul_int8_np
+    A = np.array([[[1, 2], [-3, 1]], [[100, 100], [-100, 100]]], np.int8)  # [2][2][2]
+    B = np.array([[[3, 0], [4, 1]], [[127, -128], [127, 0]]], np.int8)     # [2][2][2]
+    # batch 0 acc = [[11, 2], [-5, 1]]; bias [0.5, -0.5]; alpha = 1 * 2 / 4
+    C, _ = dnnl_matmul_int8_np(A, B, 1.0, 2.0, 4.0, np.array([0.5, -0.5], np.float32))
+    # (11.5) * 0.5 = 5.75 -> 6; (1.5) * .5 = .75 -> 1; (-4.5) * .5 = -2.25 -> -2; (.5) * .5 -> 0
+    np.testing.assert_array_equal(C[0], [[6, 1], [-2, 0]])
+    # batch 1 acc = [[25400, -12800], [0, 12800]]: saturates; (0 + .5) * .5 -> 0
+    np.testing.assert_array_equal(C[1], [[127, -128], [0, 127]])
+    C, _ = dnnl_matmul_int8_np(A[:1], B[:1], 1.0, 1.0, 2.0)   # halves: 5.5 -> 6 (even), 1 -> 1, -2.5 -> -2, .5 -> 0
+    np.testing.assert_array_equal(C[0], [[6, 1], [-2, 0]])
+    C, _ = dnnl_matmul_int8_np(A[:1], B[:1], 1.0, 1.0, 1.0, activation="relu")
+    np.testing.assert_array_equal(C[0], [[11, 2], [0, 1]])
+    C, _ = dnnl_matmul_int8_np(A[:1], B[:1], 1.0, 1.0, 1.0, activation="gelu")
+    from math import erf
+    g = lambda x: 0.5 * x * (1 + erf(x / np.sqrt(2)))
+    np.testing.assert_array_equal(C[0], np.rint([[g(11), g(2)], [g(-5), g(1)]]).astype(np.int8))
+
+
 def test_oracle_embedding_matches_reference():
     z = np.load(GOLDEN / "embed_v50.npz")
     np.testing.assert_array_equal(z["emb"][z["ids"]], z["out"])
