@@ -504,6 +504,404 @@ void pa_split_kernel(PaSplitArgs a) {
   }
 }
 
+#if LLM_TUNING
+// Tuning build only (LLM_BEAM_MFMA=1): measured slower than the VALU BEAM form
+// it was written to replace (69.8 vs 60.8 us per C4 launch;
+// loads alone 60.2 us, processing alone 48.3 us, both bound by what 2 waves
+// per SIMD keep in flight).  Parity-green (fp32-grade against float64).
+//
+// MFMA beam-group kernel (row_group 4, fp16 KV, D 128, page 16): the 4 beams
+// of a sequence for one (head, split) in one workgroup, as pa_split_kernel's
+// BEAM form, but the q.k and p.v products run on the matrix cores, so a page
+// costs the same few instructions whether it serves 1 beam or 4 (the VALU form
+// spends 4 waves x ~90 instructions on every shared page: VALU/issue-bound,
+// VERDICT r1).  Per page (16 tokens):
+//   S^T[token][c] = K[token][:] . Qc[:]   4 x v_mfma_f32_16x16x32_f16; columns
+//       c = b (beam b, q rounded to fp16) and c = 4 + b (the fp16 residual of
+//       beam b's q, scaled by 2^13), summed with one lane shift: fp32-grade scores from
+//       fp16 operands (K is fp16; products are exact in fp32)
+//   online softmax per beam column in fp32 (the C layout puts a beam's 16
+//       scores in 4 lanes x 4 registers)
+//   O^T[d][c] += V^T[d][token] . P^T[token][c]   8 x v_mfma_f32_16x16x16_f16;
+//       P^T is the score tile itself (same lanes: no movement), column b holding
+//       fp16(p), column 4 + b the fp16 residual of p (summed once at the end);
+//       V^T comes from a per-wave LDS image of the page read with
+//       ds_read_b64_tr_b16 (the hardware transpose read), XOR-swizzled rows
+// The 4 waves take the split's work items round-robin: a page all 4 beams
+// share (leading shared run, as the BEAM form) is one item for all 4 beam
+// columns; a beam-private page is one item masked to its beam.  Each item is
+// loaded once, 1 KiB contiguous per instruction, into registers (two items in
+// flight per wave), then into the wave's swizzled LDS images of K (read back
+// as MFMA rows) and V (read back transposed).  The 4 waves' (m, l, acc) per beam
+// are combined through LDS in a fixed order and written as the split's
+// partial, which pa_merge_row_kernel consumes exactly as the VALU form's.
+// Rows of a workgroup whose contexts differ (or that do not exist) fall back
+// to one wave per beam with its own pages (items masked to that beam).
+__device__ __forceinline__ uint32_t beam_lds_off(int row, int ch) {
+  // 256-byte token rows, 16-byte chunk ch: XOR swizzle so the transposed reads
+  // (4 rows x 32 bytes per 16-lane group) spread over the banks
+  return (uint32_t)(256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))));
+}
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// Maximum over each 16-lane row (DPP, every lane of the row gets it).
+__device__ __forceinline__ float row_max16(float x) {
+  x = fmaxf(x, mov_dpp<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = fmaxf(x, mov_dpp<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = fmaxf(x, mov_dpp<0x141>(x));  // row_half_mirror
+  return fmaxf(x, mov_dpp<0x140>(x));  // row_mirror
+}
+// The residual columns carry (x - fp16(x)) * 2^13: unscaled they would sit
+// below fp16's normal range (~1e-5 for q, p * 2^-12 for the weights) and
+// lose bits as subnormals.  Exact power-of-two scaling; |x| < 8192 keeps the
+// scaled residual finite.  Measured against float64
+// (scripts/debug_beam_mfma.py): 1.4e-7 .. 6.5e-7, as the VALU kernel.
+// Values below fp16's smallest normal go to the residual column whole.
+constexpr float kLoScale = 8192.f, kLoUnscale = 1.f / 8192.f;
+constexpr float kF16MinNormal = 6.103515625e-05f;
+
+// DBG (tuning build only): 1 = loads with a trivial consumer, 2 = processing
+// with no loads (zero pages)
+template <int DBG = 0>
+__global__ __launch_bounds__(256) void pa_beam_mfma_kernel(PaSplitArgs a) {
+  constexpr int D = 128, TS = 16;
+  constexpr int PAGE_BYTES = TS * D * 2;  // 4 KiB
+  __shared__ __attribute__((aligned(16))) uint8_t vimg[4][PAGE_BYTES];  // per wave
+  __shared__ __attribute__((aligned(16))) uint8_t kimg[4][PAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) _Float16 pimg[4][16 * 16];
+  __shared__ int pid_lds[4][kMaxPps];
+  __shared__ int pfx_lds[4][64];
+
+  const int lane = lane_id();
+  const int w = wave_id_uniform();
+  const int s = blockIdx.x % a.nsplit;
+  const int gh = blockIdx.x / a.nsplit;
+  const int h = gh % a.H;
+  const int g0 = (gh / a.H) * 4;
+  const int b = g0 + w;  // this wave's beam row
+  const bool brow = b < a.B;
+
+  // share: all 4 rows exist, route to valid page-table rows and hold equal
+  // contexts (uniform over the workgroup)
+  bool share = true;
+  int T0 = -1;
+  for (int i = 0; i < 4; ++i) {
+    const int bi = g0 + i;
+    if (bi >= a.B) { share = false; break; }
+    const int ri = a.beam_ids ? a.beam_ids[bi] : bi;
+    int Ti = a.context_lens ? a.context_lens[bi] : a.T;
+    Ti = min(max(Ti, 0), a.T);
+    if (ri < 0 || ri >= a.num_beams || (i > 0 && Ti != T0)) { share = false; break; }
+    T0 = Ti;
+  }
+  const int r = brow ? (a.beam_ids ? a.beam_ids[b] : b) : -1;
+  int Tb = brow ? (a.context_lens ? a.context_lens[b] : a.T) : 0;
+  Tb = min(max(Tb, 0), a.T);
+  const int ntiles = min((Tb + TS - 1) / TS, a.max_tiles);
+  int tile0, count;
+  {
+    const int pps = row_pps(a.pps, a.nsplit, ntiles);
+    tile0 = s * pps;
+    count = min(pps, ntiles - tile0);
+  }
+  const int32_t* prow =
+      (r >= 0 && r < a.num_beams) ? a.page_table + ((size_t)r * a.H + h) * a.max_tiles : nullptr;
+  if (share && a.balance16 >= 16 && a.pps == 0 && a.nsplit > 1 && ntiles > 0) {
+    // cost-balanced split boundaries over the group's shared prefix (every
+    // input uniform: all splits of the group derive the same partition)
+    int nsh_t = 0;
+    for (int blk = 0;; blk += 64) {
+      const int t = blk + lane;
+      int id = -1;
+      if (t < ntiles) {
+        id = prow[t];
+        if (id >= a.num_pages) id = -1;
+      }
+      pfx_lds[w][lane] = id;
+      __syncthreads();
+      const bool eq = t < ntiles && pfx_lds[0][lane] == pfx_lds[1][lane] &&
+                      pfx_lds[0][lane] == pfx_lds[2][lane] && pfx_lds[0][lane] == pfx_lds[3][lane];
+      const uint64_t mk = __ballot(eq);
+      __syncthreads();
+      const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
+      nsh_t = blk + run;
+      if (run < 64 || blk + 64 >= ntiles) break;
+    }
+    nsh_t = min(nsh_t, ntiles);
+    if (nsh_t > 0 && nsh_t < ntiles) {
+      const long long A = 16, P = a.balance16, ns = a.nsplit;
+      const long long C = A * nsh_t + P * (ntiles - nsh_t);
+      auto start = [&](int k) -> int {
+        if (k <= 0) return 0;
+        if (k >= ns) return ntiles;
+        const long long x = (C * k + ns - 1) / ns;
+        if (x <= A * nsh_t) return (int)((x + A - 1) / A);
+        return (int)min<long long>(ntiles, nsh_t + (x - A * nsh_t + P - 1) / P);
+      };
+      if ((C + ns - 1) / ns / A + 2 <= kMaxPps) {
+        tile0 = start(s);
+        count = start(s + 1) - tile0;
+      }
+    }
+  }
+  count = max(count, 0);
+
+  // this split's page ids of every beam row of the group (-1: missing)
+  for (int j = lane; j < kMaxPps; j += 64) {
+    int id = -1;
+    if (prow && j < count) {
+      id = prow[tile0 + j];
+      if (id >= a.num_pages) id = -1;
+    }
+    pid_lds[w][j] = id;
+  }
+  __syncthreads();
+
+  // work items of this wave
+  int nsh = 0, nitems, it0, istep;
+  if (share) {
+    while (nsh < count && pid_lds[0][nsh] == pid_lds[1][nsh] && pid_lds[0][nsh] == pid_lds[2][nsh] &&
+           pid_lds[0][nsh] == pid_lds[3][nsh])
+      ++nsh;
+    nitems = nsh + 4 * (count - nsh);
+    it0 = w;
+    istep = 4;
+  } else {
+    nitems = count;
+    it0 = 0;
+    istep = 1;
+  }
+  nsh = __builtin_amdgcn_readfirstlane(nsh);
+  // item -> (tile j, page, beam mask)
+  auto item = [&](int i, int& j, int& pg, int& mask) {
+    if (i >= nitems) { j = 0; pg = -1; mask = 0; return; }
+    if (!share) { j = i; pg = pid_lds[w][j]; mask = 1 << w; return; }
+    if (i < nsh) { j = i; pg = pid_lds[0][j]; mask = 0xF; return; }
+    const int i2 = i - nsh;
+    const int bb = i2 & 3;
+    j = nsh + (i2 >> 2);
+    pg = pid_lds[bb][j];
+    mask = 1 << bb;
+  };
+
+  // q operands (A of the score MFMAs, rows = beams): lane row c = lane & 15,
+  // c < 4: beam g0 + c, other rows 0; qh = fp16(q), ql = its fp16 residual
+  // (scaled); k-step kk holds dims 32 kk + 8 (lane >> 4) .. + 7 (the K
+  // operand's k order)
+  const int col = lane & 15;
+  const int lgrp = lane >> 4;
+  f16x8 qh[4], ql[4];
+  {
+    const int qb = g0 + col;
+    const bool qok = col < 4 && qb < a.B;
+    const float* qp = a.q + (size_t)(qok ? qb : 0) * a.q_stride + (size_t)h * D;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = qok ? qp[32 * kk + 8 * lgrp + e] * a.qscale : 0.f;
+        const _Float16 hi = fabsf(v) >= kF16MinNormal ? (_Float16)v : (_Float16)0.f;
+        qh[kk][e] = hi;
+        ql[kk][e] = (_Float16)((v - (float)hi) * kLoScale);
+      }
+    }
+  }
+
+  // online-softmax state of beam r in register r (lanes 0..15, identical)
+  float m4[4], l4[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m4[r] = kNegSentinel;
+    l4[r] = 0.f;
+  }
+  f32x4 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // P^T image of the wave: rows = beam columns (0..3 fp16(p), 4..7 residual,
+  // 8..15 zero) x 16 tokens
+  _Float16* pw = pimg[w];
+  for (int i2 = 128 + lane; i2 < 256; i2 += 64) pw[i2] = (_Float16)0.f;
+  uint8_t* vw = vimg[w];
+  uint8_t* kw = kimg[w];
+
+  struct Stage {
+    u32x4 k[4], v[4];
+  };
+  auto issue = [&](Stage& st, int i) {
+    int j, pg, mask;
+    item(i, j, pg, mask);
+    const bool ok = pg >= 0 && DBG != 2;
+    const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
+    const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k_pool + off), (short)0,
+                                                       ok ? PAGE_BYTES : 0, 0x00020000);
+    const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.v_pool + off), (short)0,
+                                                       ok ? PAGE_BYTES : 0, 0x00020000);
+    // K and V: linear 1 KiB per instruction (token 4 c + lgrp, chunk col)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      st.k[c] = __builtin_amdgcn_raw_buffer_load_b128(krs, (uint32_t)(c * 1024 + lane * 16), 0,
+                                                       kKvLoadAux);
+      st.v[c] = __builtin_amdgcn_raw_buffer_load_b128(vrs, (uint32_t)(c * 1024 + lane * 16), 0,
+                                                       kKvLoadAux);
+    }
+  };
+  auto process = [&](const Stage& st, int i) {
+    if constexpr (DBG == 1) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) x ^= st.k[c][0] ^ st.v[c][3];
+      acc[0][0] += (float)(x & 1u);
+      return;
+    }
+    int j, pg, mask;
+    item(i, j, pg, mask);
+    const bool ok = pg >= 0;
+    const int tok0 = (tile0 + j) * TS;
+    // FULL (uniform): the page is present and all 16 tokens are inside the
+    // context: no per-token masks (all pages of a row but its last)
+    const bool full = ok && tok0 + TS <= Tb;
+    // K and V images (V rows past the context or of a missing page: zeros,
+    // so stale NaN / Inf cannot reach the MFMA; such K rows are masked)
+    if (full) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        *reinterpret_cast<u32x4*>(kw + beam_lds_off(4 * c + lgrp, col)) = st.k[c];
+        *reinterpret_cast<u32x4*>(vw + beam_lds_off(4 * c + lgrp, col)) = st.v[c];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int row = 4 * c + lgrp;
+        const bool vok = ok && tok0 + row < Tb;
+        *reinterpret_cast<u32x4*>(kw + beam_lds_off(row, col)) = st.k[c];
+        *reinterpret_cast<u32x4*>(vw + beam_lds_off(row, col)) =
+            vok ? st.v[c] : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    // scores S[beam r][token] in lanes 0..15 (token = lane), register r:
+    // A = q rows, B = K^T (token column col, dims 32 kk + 8 lgrp .. + 7)
+    f32x4 sh = f32x4{0.f, 0.f, 0.f, 0.f}, sl = sh;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const f16x8 kf = __builtin_bit_cast(
+          f16x8, *reinterpret_cast<const u32x4*>(kw + beam_lds_off(col, 4 * kk + lgrp)));
+      sh = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[kk], kf, sh, 0, 0, 0);
+      sl = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[kk], kf, sl, 0, 0, 0);
+    }
+    // per-beam online softmax: the 16 tokens of beam r sit in one DPP row
+    const bool tok_ok = lane < 16 && (full || (ok && tok0 + lane < Tb));
+    float p[4], corr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool valid = tok_ok && ((mask >> r) & 1);
+      const float sv = valid ? sh[r] + sl[r] * kLoUnscale : kNegSentinel;
+      const float mnew = fmaxf(m4[r], row_max16(sv));
+      corr[r] = __builtin_amdgcn_exp2f(m4[r] - mnew);
+      p[r] = valid ? __builtin_amdgcn_exp2f(sv - mnew) : 0.f;
+      l4[r] = l4[r] * corr[r] + group_sum<16>(p[r]);
+      m4[r] = mnew;
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const _Float16 hi = p[r] >= kF16MinNormal ? (_Float16)p[r] : (_Float16)0.f;
+        pw[r * 16 + lane] = hi;
+        pw[(4 + r) * 16 + lane] = (_Float16)((p[r] - (float)hi) * kLoScale);
+      }
+    }
+    // rescale the accumulators only when some beam's maximum moved (after the
+    // first pages of a split, almost never): corr is exactly 1 otherwise
+    if (__ballot(corr[0] != 1.f || corr[1] != 1.f || corr[2] != 1.f || corr[3] != 1.f)) {
+      const float c0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(corr[0]), 0));
+      const float c1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(corr[1]), 0));
+      const float c2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(corr[2]), 0));
+      const float c3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(corr[3]), 0));
+      const int bcol = col & 3;
+      const float cc = bcol == 0 ? c0 : bcol == 1 ? c1 : bcol == 2 ? c2 : c3;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] *= cc;
+    }
+    // P^T operand: beam column col, tokens 4 lgrp .. + 3
+    const f16x4 pf = *reinterpret_cast<const f16x4*>(pw + col * 16 + 4 * lgrp);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      // V^T operand of dims 16 i .. 16 i + 15: lane 4 qq + pp of group lgrp
+      // addresses token row 4 lgrp + qq, dims 16 i + 4 pp .. + 3
+      const int qq = col >> 2, pp = col & 3;
+      const uint32_t ad = beam_lds_off(4 * lgrp + qq, 2 * i + (pp >> 1)) + 8 * (pp & 1);
+      const s16x4 vt = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(vw + ad));
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(f16x4, vt), pf, acc[i],
+                                                      0, 0, 0);
+    }
+  };
+
+  {
+    Stage sa, sb;
+    int i = it0;
+    issue(sa, i);
+    while (i < nitems) {
+      issue(sb, i + istep);  // past the end: nothing loaded (num_records 0)
+      process(sa, i);
+      i += istep;
+      if (i >= nitems) break;
+      issue(sa, i + istep);
+      process(sb, i);
+      i += istep;
+    }
+  }
+
+  // beam column b: fp16 part + residual part (columns b and b + 4)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[i][q] += __shfl_down(acc[i][q], 4, 16) * kLoUnscale;
+
+  // combine the 4 waves' states per beam through LDS (each wave reuses its own
+  // V image: acc [beam][128] then (m, l) [beam][2])
+  float* red = reinterpret_cast<float*>(vw);
+  if (col < 4) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[col * D + 16 * i + 4 * lgrp + q] = acc[i][q];
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[4 * D + 2 * r] = m4[r];
+        red[4 * D + 2 * r + 1] = l4[r];
+      }
+    }
+  }
+  __syncthreads();
+  if (brow) {
+    float mv[4], M = kNegSentinel;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      mv[v] = reinterpret_cast<const float*>(vimg[v])[4 * D + 2 * w];
+      M = fmaxf(M, mv[v]);
+    }
+    float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float* rv = reinterpret_cast<const float*>(vimg[v]);
+      const float e = __builtin_amdgcn_exp2f(mv[v] - M);
+      L += rv[4 * D + 2 * w + 1] * e;
+      o0 += rv[w * D + 2 * lane] * e;
+      o1 += rv[w * D + 2 * lane + 1] * e;
+    }
+    const size_t pidx = ((size_t)b * a.H + h) * a.nsplit + s;
+    *reinterpret_cast<float2*>(a.part_acc + pidx * D + 2 * lane) = float2{o0, o1};
+    if (lane == 0) {
+      a.part_ml[pidx * 2] = M;
+      a.part_ml[pidx * 2 + 1] = L;
+    }
+  }
+}
+#endif  // LLM_TUNING
+
 // sum_s part[s * stride] * w_s over s < ns with w_s held by lane s (s < 64) /
 // lane s - 64 of w1: loads issued 8 splits at a time so a merge costs a few
 // memory round trips, not one per split; summation order s = 0, 1, ...
@@ -736,6 +1134,26 @@ long long resident_waves() {
   return cached;
 }
 
+// The MFMA beam-group kernel (D 128, page 16) exists only in the tuning build
+// (LLM_BEAM_MFMA=1).  A private page costs it 4 items to a shared page's 1:
+// split balance 64/16.
+bool beam_mfma_on() {
+#if LLM_TUNING
+  static const bool v = env_int("LLM_BEAM_MFMA", 0) != 0;
+  return v;
+#else
+  return false;
+#endif
+}
+int beam_mfma_balance16() {
+#if LLM_TUNING
+  static const int v = env_int("LLM_BEAM_MFMA_BALANCE16", 64);
+  return v >= 16 ? v : 0;
+#else
+  return 64;
+#endif
+}
+
 // lean = the low-register form (one 8 KiB register stage, 8 waves per SIMD
 // requested): same stream rate measured (scripts/tune_attention.py variant 6
 // vs 1), used when the launch must leave CU room for kernels running beside
@@ -765,6 +1183,23 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
 #ifndef LLM_BEAM_CHUNK
 #define LLM_BEAM_CHUNK 8192
 #define LLM_BEAM_WAVES 0
+#endif
+#if LLM_TUNING
+    if constexpr (D == 128 && TS == 16) {
+      if (beam_mfma_on()) {
+        PaSplitArgs am = a;
+        am.balance16 = beam_mfma_balance16();
+        static const int dbg = env_int("LLM_BEAM_MFMA_DBG", 0);
+        if (dbg == 1)
+          hipLaunchKernelGGL(pa_beam_mfma_kernel<1>, grid, block, 0, st, am);
+        else if (dbg == 2)
+          hipLaunchKernelGGL(pa_beam_mfma_kernel<2>, grid, block, 0, st, am);
+        else
+        hipLaunchKernelGGL(pa_beam_mfma_kernel<0>, grid, block, 0, st, am);
+        *beam = true;
+        return hipGetLastError();
+      }
+    }
 #endif
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
                                         false, true>), grid, block, 0, st, a);
@@ -976,6 +1411,17 @@ int beam_balance16() {
 #endif
 }
 
+template <int D, int TS>
+hipError_t beam_occupancy(int* blocks) {
+#if LLM_TUNING
+  if (D == 128 && TS == 16 && beam_mfma_on())
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, pa_beam_mfma_kernel<0>, 256, 0);
+#endif
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      blocks, pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true>,
+      256, 0);
+}
+
 // Resident waves of the beam-group kernel (0 where the plain schedule runs
 // instead: pages above 8 KiB).
 template <int D, int TS>
@@ -989,10 +1435,7 @@ long long beam_resident_waves() {
     cached = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &blocks,
-            pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true>,
-            256, 0) == hipSuccess &&
+        beam_occupancy<D, TS>(&blocks) == hipSuccess &&
         cus > 0 && blocks > 0)
       cached = (long long)cus * blocks * 4;
     else

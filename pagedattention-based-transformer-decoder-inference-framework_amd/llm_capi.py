@@ -222,11 +222,12 @@ def kv_view(k_pool, v_pool, page_table, *, num_beams=None) -> PaKvView:
 
 
 def pa_decode(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_lens=None,
-              sm_scale=1.0, pages_per_split=0, out=None, stream=None, row_group=1):
+              sm_scale=1.0, pages_per_split=0, out=None, stream=None, row_group=1, lib=None):
     """Paged decode attention on torch device tensors; returns out [B][H][D] fp32.
-    row_group > 1 uses the beam-aware schedule (pa_decode_grouped)."""
+    row_group > 1 uses the beam-aware schedule (pa_decode_grouped).  lib: the
+    library to call (default the product build; load_tune() for variant tests)."""
     import torch
-    lib = load()
+    lib = lib or load()
     B, H, D = q.shape
     if out is None:
         out = torch.empty((B, H, D), dtype=torch.float32, device=q.device)

@@ -81,3 +81,83 @@ def test_c4_beam_group_attention_vs_oracle(gpu, oracle, layer):
         ref = oracle.paged_attention(qh[row:row + 1, head:head + 1], kk, vv, sub_pt, T=T)
         assert rel_err(outs[W][row, head], ref[0, 0]) < 1e-3, (row, head)
         assert rel_err(outs[1][row, head], ref[0, 0]) < 1e-3, (row, head)
+
+
+@pytest.mark.parametrize("B,T,shared,equal", [
+    (6, 700, 30, True),    # a full group and a 2-row group (no sharing in the second)
+    (8, 5, 1, True),       # context inside the first page, most splits empty
+    (12, 330, 20, False),  # ragged contexts: one wave per beam, own pages
+    (8, 4096, 240, True),  # C4 shape per sequence, 2 sequences
+])
+def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal):
+    """The beam-group attention launch (row_group 4, fp16, D 128, page 16) on
+    the cases its schedule branches on: partial groups, sub-page contexts and
+    empty splits, ragged contexts, beam_ids routing inside a group, a missing
+    shared page, and never-written (NaN) token rows past every context in both
+    shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
+    cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1)."""
+    import torch
+    import llm_capi
+    rng = np.random.default_rng(B * 7 + T)
+    H, D, ts, W = 3, 128, 16, 4
+    nt = (T + ts - 1) // ts
+    shared = min(shared, nt)
+    seqs = (B + W - 1) // W
+    num_pages = seqs * H * shared + B * H * (nt - shared) + 2
+    perm = rng.permutation(num_pages).astype(np.int32)
+    pt = np.full((B, H, nt), -1, np.int32)
+    i = 0
+    for sq in range(seqs):
+        blk = perm[i:i + H * shared].reshape(H, shared)
+        i += H * shared
+        for w in range(W):
+            if sq * W + w < B:
+                pt[sq * W + w, :, :shared] = blk
+    for b in range(B):
+        pt[b, :, shared:] = perm[i:i + H * (nt - shared)].reshape(H, nt - shared)
+        i += H * (nt - shared)
+    if shared > 2:
+        pt[0:W, 1, 2] = -1  # a missing shared page
+    if equal:
+        lens = np.repeat(rng.integers(max(1, T - 40), T + 1, size=seqs), W)[:B].astype(np.int32)
+    else:
+        lens = rng.integers(1, T + 1, size=B).astype(np.int32)
+    kp = (rng.standard_normal((num_pages, ts, D)) * D ** -0.25).astype(np.float16)
+    vp = rng.standard_normal((num_pages, ts, D)).astype(np.float16)
+    # never-written rows: NaN past each row's context in its last page (only
+    # where no other row of the group reads those tokens: equal contexts, or a
+    # private page)
+    for b in range(B):
+        t = int(lens[b])
+        if t % ts and (equal or t // ts >= shared):
+            for h in range(H):
+                pg = pt[b, h, t // ts]
+                if pg >= 0:
+                    kp[pg, t % ts:] = np.nan
+                    vp[pg, t % ts:] = np.nan
+    # beam_ids: rows of a group read their page-table rows in a permuted order
+    beam_ids = np.arange(B, dtype=np.int32)
+    beam_ids[:W] = [1, 3, 0, 2][:min(W, B)]
+    q = (rng.standard_normal((B, H, D)) * D ** -0.25).astype(np.float32)
+    d = lambda a: torch.from_numpy(a).cuda()
+    kf = np.nan_to_num(kp.astype(np.float32), nan=0.0)
+    vf = np.nan_to_num(vp.astype(np.float32), nan=0.0)
+    ref = oracle.paged_attention(q, kf, vf, pt, T=T, context_lens=lens, beam_ids=beam_ids)
+    plain = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                               beam_ids=d(beam_ids)).cpu().numpy()
+    outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                              beam_ids=d(beam_ids), row_group=4).cpu().numpy()
+    assert np.isfinite(outg).all()
+    assert rel_err(plain, ref) < 1e-3
+    assert rel_err(outg, ref) < 1e-3
+    assert rel_err(outg, plain) < 1e-5
+    # the tuning build's MFMA beam kernel (not in the product library; its
+    # switch is read once per process, before the tuning build's first launch)
+    import os
+    os.environ["LLM_BEAM_MFMA"] = "1"
+    outm = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                              beam_ids=d(beam_ids), row_group=4,
+                              lib=llm_capi.load_tune()).cpu().numpy()
+    assert np.isfinite(outm).all()
+    assert rel_err(outm, ref) < 1e-3
+    assert rel_err(outm, plain) < 1e-5
