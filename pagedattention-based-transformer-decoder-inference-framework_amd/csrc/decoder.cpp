@@ -107,6 +107,7 @@ struct llm_decoder {
   // the GEMM's epilogue by the next LayerNorm launch (pending describes them)
   DevBuf<int32_t> part;
   LnPartials pending;
+  LnPartials embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
   bool split_k(const struct Rows& R, int N, int K) const;
 
   ~llm_decoder() {
@@ -132,7 +133,8 @@ struct llm_decoder {
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
   int step_tail(hipStream_t st, int r0, int n);
-  int next_tokens(const float* xr, int n, int r0, const int32_t* ctr, hipStream_t st);
+  int next_tokens(const float* xr, int n, int r0, const int32_t* ctr, hipStream_t st,
+                  int32_t* adv_pos = nullptr, int32_t* adv_ctx = nullptr);
   int enqueue_step(hipStream_t st);
   int run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host, hipStream_t st);
 
@@ -378,20 +380,23 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
 // launch writing the packed A the GEMM reads.
 int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamma,
                                  const float* beta, hipStream_t st) {
+  // the step's first LayerNorm reads the token embedding rows (step_head)
+  const LnPartials src = embed_src.emb ? embed_src : pending;
+  embed_src = LnPartials{};
   if (R.prefill_row < 0 && ln_fusable(wdtype, R.n, hid)) {
     g.ln_x = R.x; g.ln_g = gamma; g.ln_b = beta; g.ln_eps = 1e-5f;
+    g.ln_emb = src.emb; g.ln_tok = src.tok; g.ln_V = src.V;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
     return LLM_OK;
   }
-  if (wdtype == LLM_I8) {
-    // a pending split-K result is summed (and its rows stored to x) first
-    const LnPartials* pp = pending.part ? &pending : nullptr;
+  // a pending split-K result is summed (and its rows stored to x) first
+  const LnPartials* pp = src.part || src.emb ? &src : nullptr;
+  if (wdtype == LLM_I8)
     LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, gamma, beta, 1e-5f, nullptr,
                                        static_cast<int8_t*>(R.act), R.sa, st, 1, pp));
-    pending = LnPartials{};
-  } else {
-    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, gamma, beta, 1e-5f, R.act, st, 1));
-  }
+  else
+    LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, gamma, beta, 1e-5f, R.act, st, 1, pp));
+  pending = LnPartials{};
   return LLM_OK;
 }
 
@@ -472,7 +477,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   }
   RET_IF(weight_gemm(g, st));
   if (i8) RET_IF(tap(l, 2, R, hid, st));
-  g.ln_x = nullptr; g.act_out = nullptr; g.sa_out = nullptr;
+  g.ln_x = nullptr; g.ln_emb = nullptr; g.act_out = nullptr; g.sa_out = nullptr;
   g.C16 = nullptr;
   if (!i8) g.A = R.act2;
   // quantise h1 -> mlp_fc2 (+b2)
@@ -528,35 +533,45 @@ int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
 // LM head + token choice for rows r0.. (x rows given): logits into the step's
 // logits buffer; greedy ids from the LM head's fused argmax partials, or a
 // device draw (sample_rows) with the rows' positions as draw counters.
-int llm_decoder::next_tokens(const float* xr, int n, int r0, const int32_t* ctr, hipStream_t st) {
+// adv_pos / adv_ctx (optional): advance the rows' positions afterwards (fused
+// into the argmax launch; a launch of its own after a draw, which reads them).
+int llm_decoder::next_tokens(const float* xr, int n, int r0, const int32_t* ctr, hipStream_t st,
+                             int32_t* adv_pos, int32_t* adv_ctx) {
   float* lg = logits.p + (size_t)r0 * V;
   const bool sample = temperature > 0.f && top_k != 1;
   float* pv = lm_pv.p + (size_t)r0 * lm_nwg;
   int32_t* pi = lm_pi.p + (size_t)r0 * lm_nwg;
   LLM_HIP_RET(launch_lm_head(xr, emb_packed.p, lg, n, V, hid, sample ? nullptr : pv, pi, st));
-  if (sample)
+  if (sample) {
     LLM_HIP_RET(launch_sample(lg, n, r0, V, temperature, top_k, top_p, sample_seed, ctr,
                               tokens.p + r0, st));
-  else
-    LLM_HIP_RET(launch_argmax_partials(pv, pi, n, lm_nwg, tokens.p + r0, st));  // in place
+    if (adv_pos) LLM_HIP_RET(launch_advance(adv_pos, adv_ctx, n, st));
+  } else {
+    LLM_HIP_RET(launch_argmax_partials(pv, pi, n, lm_nwg, tokens.p + r0, st, adv_pos, adv_ctx));
+  }
   return LLM_OK;
 }
 
+// The step's embedding: no launch of its own; layer 0's first LayerNorm
+// (launch or GEMM prologue) reads E[token] rows directly (embed_src).
 int llm_decoder::step_head(hipStream_t st, int r0, int n) {
-  return launch_embed(emb.p, tokens.p + r0, n, hid, V, x.p + (size_t)r0 * hid, st) == hipSuccess
-             ? LLM_OK
-             : fail(LLM_ERR_HIP, "embed launch");
+  (void)st;
+  embed_src = LnPartials{};
+  embed_src.emb = reinterpret_cast<const _Float16*>(emb.p);
+  embed_src.tok = tokens.p + r0;
+  embed_src.V = V;
+  (void)n;
+  return LLM_OK;
 }
 
 int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
-  RET_IF(next_tokens(x.p + (size_t)r0 * hid, n, r0, pos.p + r0, st));
-  LLM_HIP_RET(launch_advance(pos.p + r0, ctx.p + r0, n, st));
-  return LLM_OK;
+  return next_tokens(x.p + (size_t)r0 * hid, n, r0, pos.p + r0, st, pos.p + r0, ctx.p + r0);
 }
 
 // One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
   const Rows R = step_rows(0, batch, attn_ws.p);
+  pending = LnPartials{};
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -682,6 +697,8 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     R.prefill_p0 = p0;
     R.attn_ws = pws.p; R.attn_ws_bytes = pws_bytes;
     LLM_HIP_RET(launch_embed(emb.p, pmeta.p + 3 * C, m, hid, V, px.p, st));
+    embed_src = LnPartials{};  // (a failed step enqueue could have left either set)
+    pending = LnPartials{};
     for (int l = 0; l < L; ++l) {
       RET_IF(layer_pre(l, st, R));
       RET_IF(layer_attn(l, st, R));

@@ -63,6 +63,9 @@ struct GemmArgs {
   // per row, scales kept in LDS for the epilogue), computed by every workgroup
   // for its own rows into LDS instead of read from a LayerNorm launch's output
   const float* ln_x;      // [M][K] fp32
+  const _Float16* ln_emb; // or rows E[ln_tok[m]] (fp16 [V][K])
+  const int32_t* ln_tok;
+  int ln_V;
   const float* ln_g;      // [K]
   const float* ln_b;      // [K]
   float ln_eps;
@@ -153,7 +156,12 @@ __device__ __forceinline__ void ln_prologue(const GemmArgs& a, int m0, uint8_t* 
     for (int q = 0; q < 2; ++q) {
       const int r = r0 + q * WAVES;
       const int m = m0 + r;
-      ln_wave_load(a.ln_x + (size_t)m * K, K4, r < ROWS && m < a.M, x[q]);
+      const bool ok = r < ROWS && m < a.M;
+      if (a.ln_emb)
+        ln_wave_load_f16(ok ? ln_embed_row(a.ln_emb, a.ln_tok, m, a.ln_V, K) : a.ln_emb, K4, ok,
+                         x[q]);
+      else
+        ln_wave_load(a.ln_x + (size_t)m * K, K4, ok, x[q]);
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -698,6 +706,7 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   LLM_REQUIRE(!g.C16 || g.N % 32 == 0, "weight_gemm: packed fp16 output needs N % 32 == 0");
   a.c16 = static_cast<_Float16*>(g.C16);
   a.ln_x = g.ln_x; a.ln_g = g.ln_g; a.ln_b = g.ln_b; a.ln_eps = g.ln_eps;
+  a.ln_emb = g.ln_emb; a.ln_tok = g.ln_tok; a.ln_V = g.ln_V;
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;
   if (g.partial) {

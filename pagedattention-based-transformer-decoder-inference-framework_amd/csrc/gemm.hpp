@@ -46,6 +46,9 @@ struct WeightGemm {
   // (ln_fusable); act_out / sa_out optionally receive A (packed-A order) and
   // the row scales (activation taps).  A / sa are then ignored.
   const float* ln_x = nullptr;
+  const _Float16* ln_emb = nullptr;  // optional: rows are E[ln_tok[m]] (fp16) instead of ln_x
+  const int32_t* ln_tok = nullptr;
+  int ln_V = 0;
   const float* ln_g = nullptr;
   const float* ln_b = nullptr;
   float ln_eps = 1e-5f;
@@ -60,6 +63,9 @@ struct WeightGemm {
 
 // Split-K input of a LayerNorm launch: x[m][n] = (float)(sum_z part[z][m][n])
 // * (sa[m] * sw[n]) + bias[n] -- bit for bit the GEMM epilogue it replaces.
+// Input of the LayerNorm launch when it is not x: a split-K GEMM's int32
+// partials (part != NULL), or embedding rows E[tok[r]] (emb != NULL; the
+// decode step's first LayerNorm reads the token embedding directly).
 struct LnPartials {
   const int32_t* part = nullptr;
   int slices = 0;
@@ -67,6 +73,9 @@ struct LnPartials {
   const float* sw = nullptr;
   const float* bias = nullptr;  // may be NULL
   float* x_out = nullptr;       // the reconstructed rows (fp32 [M][N])
+  const _Float16* emb = nullptr;
+  const int32_t* tok = nullptr;
+  int V = 0;
 };
 
 int weight_gemm(const WeightGemm& g, hipStream_t st);

@@ -203,9 +203,13 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
 }
 
 // Per row: the first maximum over the workgroup partials (in vocabulary order).
+// pos / ctx (optional): the decode step's position advance of the row, fused
+// here instead of a launch of its own.
 __global__ __launch_bounds__(256) void argmax_partials_kernel(const float* __restrict__ pv,
                                                               const int32_t* __restrict__ pi,
-                                                              int nwg, int32_t* __restrict__ out) {
+                                                              int nwg, int32_t* __restrict__ out,
+                                                              int32_t* __restrict__ pos,
+                                                              int32_t* __restrict__ ctx) {
   __shared__ float sv[4];
   __shared__ int si[4];
   const int r = blockIdx.x;
@@ -230,6 +234,10 @@ __global__ __launch_bounds__(256) void argmax_partials_kernel(const float* __res
     for (int k = 1; k < 4; ++k)
       if (sv[k] > bv || (sv[k] == bv && si[k] < bi)) { bv = sv[k]; bi = si[k]; }
     out[r] = bi == 0x7fffffff ? 0 : bi;
+    if (pos) {
+      pos[r] += 1;
+      ctx[r] += 1;
+    }
   }
 }
 
@@ -286,9 +294,9 @@ hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, i
 }
 
 hipError_t launch_argmax_partials(const float* part_val, const int32_t* part_idx, int M, int nwg,
-                                  int32_t* out, hipStream_t st) {
+                                  int32_t* out, hipStream_t st, int32_t* pos, int32_t* ctx) {
   hipLaunchKernelGGL(argmax_partials_kernel, dim3(M), dim3(256), 0, st, part_val, part_idx, nwg,
-                     out);
+                     out, pos, ctx);
   return hipGetLastError();
 }
 

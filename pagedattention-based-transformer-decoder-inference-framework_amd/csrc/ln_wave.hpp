@@ -49,6 +49,30 @@ __device__ __forceinline__ void ln_wave_load(const float* __restrict__ row, int 
   }
 }
 
+// The same chunks from an fp16 row (an embedding row: TokenEmbedding::forward,
+// decoder/token_embedding.hpp:19-26, widened exactly).
+template <int CPL>
+__device__ __forceinline__ void ln_wave_load_f16(const _Float16* __restrict__ row, int K4, bool ok,
+                                                 LnRow<CPL>& r) {
+  const int lane = lane_id();
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4* row4 = reinterpret_cast<const h4*>(row);
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = 64 * j + lane;
+    const h4 h = (ok && c < K4) ? row4[c] : h4{0, 0, 0, 0};
+    r.v[j] = f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+}
+
+// Embedding row of token id tok (clamped to [0, V), as embed_kernel).
+__device__ __forceinline__ const _Float16* ln_embed_row(const _Float16* E, const int32_t* tok,
+                                                        int m, int V, int K) {
+  int t = tok[m];
+  t = t < 0 ? 0 : (t >= V ? V - 1 : t);
+  return E + (size_t)t * K;
+}
+
 // x -> LN(x) in place; returns the row's |max| (wave-uniform).
 template <int CPL>
 __device__ __forceinline__ float ln_wave_compute(LnRow<CPL>& x, const LnRow<CPL>& gm,

@@ -217,6 +217,18 @@ __global__ __launch_bounds__(kRowThreads) void layernorm_rows_kernel(
       const int c = threadIdx.x + i * kRowThreads;
       if (pp.x_out && c < n4) reinterpret_cast<f32x4*>(pp.x_out + (size_t)r * cols)[c] = v[i];
     }
+  } else if (pp.emb) {  // x = E[tok[r]] (embed_kernel's values, not stored)
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    const h4* er = reinterpret_cast<const h4*>(ln_embed_row(pp.emb, pp.tok, r, pp.V, cols));
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kRowThreads;
+      const bool ok = c < n4;
+      const h4 e = ok ? er[c] : h4{0, 0, 0, 0};
+      v[i] = f32x4{(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
+      gv[i] = ok ? g4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      bv[i] = ok ? b4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   } else {
     const f32x4* xr = reinterpret_cast<const f32x4*>(x + (size_t)r * cols);
 #pragma unroll
@@ -407,6 +419,7 @@ static hipError_t launch_ln(const float* x, int rows, int cols, const float* g, 
   const int v = row_vpt(cols);
   if (pp && pp->part && (v == 0 || v > 4 || pp->slices > 4)) return hipErrorInvalidValue;
   if (pack && (v == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
+  if (pp && pp->emb && v == 0) return hipErrorInvalidValue;
   if (v == 0) {  // odd widths (C ABI only)
     hipLaunchKernelGGL(layernorm_quant_kernel, dim3(rows), dim3(kRowThreads),
                        (size_t)cols * sizeof(float), st, x, cols, g, b, eps, out, q, inv, out16);
@@ -431,9 +444,10 @@ hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const floa
 }
 
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
-                                const float* b, float eps, void* out16, hipStream_t st, int pack) {
+                                const float* b, float eps, void* out16, hipStream_t st, int pack,
+                                const LnPartials* pp) {
   return launch_ln(x, rows, cols, g, b, eps, nullptr, nullptr, nullptr,
-                   static_cast<_Float16*>(out16), st, pack);
+                   static_cast<_Float16*>(out16), st, pack, pp);
 }
 
 hipError_t launch_to_f16(const float* x, size_t n, void* y, hipStream_t st, int pack_cols) {

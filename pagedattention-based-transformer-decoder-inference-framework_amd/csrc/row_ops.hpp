@@ -13,13 +13,14 @@ namespace llm {
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv,
                                 hipStream_t st, int pack = 0);
 struct LnPartials;
-// pp (optional): rebuild x from a split-K GEMM's int32 partials first (gemm.hpp)
+// pp (optional): rebuild x from a split-K GEMM's int32 partials first, or read
+// the rows as embedding rows E[tok[r]] (gemm.hpp LnPartials)
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
                                   hipStream_t st, int pack = 0, const LnPartials* pp = nullptr);
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
                                 const float* b, float eps, void* out16, hipStream_t st,
-                                int pack = 0);
+                                int pack = 0, const LnPartials* pp = nullptr);
 hipError_t launch_to_f16(const float* x, size_t n, void* y, hipStream_t st, int pack_cols = 0);
 hipError_t launch_advance(int32_t* pos, int32_t* ctx, int n, hipStream_t st);
 hipError_t launch_argmax(const float* logits, int rows, int V, int32_t* out, int32_t* out2,
@@ -36,7 +37,8 @@ hipError_t launch_lm_pack(const void* E, void* P, int V, int K, hipStream_t st);
 hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, int V, int K,
                           float* part_val, int32_t* part_idx, hipStream_t st);
 hipError_t launch_argmax_partials(const float* part_val, const int32_t* part_idx, int M, int nwg,
-                                  int32_t* out, hipStream_t st);
+                                  int32_t* out, hipStream_t st, int32_t* pos = nullptr,
+                                  int32_t* ctx = nullptr);
 // Device sampling (csrc/sample.hip); counter[r] is the per-row draw counter.
 hipError_t launch_sample(const float* logits, int rows, int row0, int V, float temperature,
                          int top_k, float top_p, uint64_t seed, const int32_t* counter,

@@ -10,13 +10,13 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
-adv = [r for r in rows if "advance_kernel" in r["Kernel_Name"]]
-nmb = len({r["Queue_Id"] for r in adv}) or 1  # micro-batches (one advance each per step)
+# the step's last kernel: the greedy argmax (which also advances the positions)
+adv = [r for r in rows if "argmax_partials_kernel" in r["Kernel_Name"]]
+nmb = len({r["Queue_Id"] for r in adv}) or 1
 adv.sort(key=lambda r: r["e"])
 t_end = adv[-1]["e"]
 t_beg = adv[-1 - nmb]["e"] if len(adv) > nmb else rows[0]["s"]
 step = [r for r in rows if r["s"] >= t_beg and r["e"] <= t_end]
-# include trailing advance kernels
 t0 = step[0]["s"]
 t1 = max(r["e"] for r in step)
 print(f"step kernels {len(step)} span {(t1 - t0) / 1e3:.1f} us, queues {sorted({r['Queue_Id'] for r in step})}")
