@@ -360,18 +360,20 @@ def _f16_reference_logits(w, tokens_per_step, oracle):
     return all_logits
 
 
-def test_cuda_decoder_fp16_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("H", [2, 12])
+def test_cuda_decoder_fp16_vs_oracle(gpu, oracle, H):
     """CUDADecoder (fp16 weights, fp16 GEMM inputs, fp16 KV) against the
     oracle's restated CUDADecoder step (oracle.cpp f16_gemm path), 24 steps of
     ragged prompts then fed-back tokens: logits within LOGIT_TOL, tokens exact
     unless the oracle's top two are within TIE_TOL.  No int8 rounding here, so
     no teacher forcing is needed (an fp16 rounding flip moves a logit ~1e-6).
-    A float64 numpy restatement (_f16_reference_logits) agrees as well."""
+    A float64 numpy restatement (_f16_reference_logits) agrees as well.
+    H 12 is C2's width (hid 768, inter 3072)."""
     torch = _torch()
     import llm_decoder
     from oracle.oracle import OracleDecoder
     rng = np.random.default_rng(9)
-    L, H, D, V, S = 2, 2, 64, 300, 40
+    L, D, V, S = 2, 64, 300, 40
     w = _f16_model(rng, L, H, D, V, S)
     c = w["cfg"]
     dec = llm_decoder.CUDADecoder(L, H, D, c["hid"], V, S, max_batch=2)
@@ -538,9 +540,11 @@ def test_prefill_decode_kernel_fallback(gpu, oracle):
     through the decode kernel, one row per prompt token (beam_ids = the row,
     context_lens = p0 + i + 1).  Against stepping the prompt token by token the
     attention split order and the fp32 order of the GEMM-fused LayerNorm differ
-    (~1e-7): the fp16 CUDADecoder (no int8 rounding to amplify it) agrees to
-    LOGIT_TOL (measured 3e-4 over 530 prompt tokens); the INT8Decoder, where such
-    a difference can flip an int8 activation, to FREE_RUN_TOL."""
+    (~1e-7): the fp16 CUDADecoder (no int8 rounding to amplify it) holds both paths to
+    LOGIT_TOL of the oracle's restated step and to each other within twice that
+    (fp16 activation roundings flip independently in the two paths); the
+    INT8Decoder, where such a difference can flip an int8 activation, to
+    FREE_RUN_TOL."""
     import llm_decoder
     rng = np.random.default_rng(4)
     L, H, D, V, S = 2, 2, 256, 400, 700
@@ -556,8 +560,15 @@ def test_prefill_decode_kernel_fallback(gpu, oracle):
 
     prompts = [rng.integers(0, V, 530).tolist(), rng.integers(0, V, 9).tolist()]
     la, lb, nxt = _prefill_vs_stepping(make_f16, prompts, V)
+    from oracle.oracle import OracleDecoder
     for r in range(2):
-        assert rel_err(lb[r], la[r]) < LOGIT_TOL, (r, rel_err(lb[r], la[r]))
+        # both paths against the oracle's restated step over the same prompt
+        od = OracleDecoder(oracle, wf, 1)
+        for i, t in enumerate(prompts[r]):
+            _, ol, _ = od.step(np.array([t], np.int32), np.array([i], np.int32))
+        assert rel_err(la[r], ol[0]) < LOGIT_TOL, (r, "prefill", rel_err(la[r], ol[0]))
+        assert rel_err(lb[r], ol[0]) < LOGIT_TOL, (r, "stepping", rel_err(lb[r], ol[0]))
+        assert rel_err(lb[r], la[r]) < 2 * LOGIT_TOL, (r, rel_err(lb[r], la[r]))
         assert la[r].max() - la[r][nxt[r]] <= LOGIT_TOL * np.abs(la[r]).max()
     w = _int8_model(oracle, L=2, H=2, D=256, V=400, S=700, seed=13)
     la, lb, nxt = _prefill_vs_stepping(lambda n: _make_gpu_decoder(w, max_batch=n), prompts, V)
