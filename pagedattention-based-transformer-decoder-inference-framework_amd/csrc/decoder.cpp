@@ -401,11 +401,12 @@ int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamm
 }
 
 // Split-K for an I8 weight GEMM of N columns whose output feeds a LayerNorm
-// launch (decode rows; not the GEMM-fused LayerNorm): the column grid alone
-// leaves CUs idle, and every workgroup then reads 1/slices of A.
+// launch (33..64 decode rows; not the GEMM-fused LayerNorm): the column grid
+// alone leaves CUs idle, and every workgroup then reads 1/slices of A.
 bool llm_decoder::split_k(const Rows& R, int N, int K) const {
-  return wdtype == LLM_I8 && R.prefill_row < 0 && R.n <= 64 && !ln_fusable(wdtype, R.n, hid) &&
-         gemm_kslices(N, R.n, K / 64) > 1;
+  // 17..32 rows take the narrow 16-row tiles instead (gemm.hip narrow_decode_tile)
+  return wdtype == LLM_I8 && R.prefill_row < 0 && R.n > 32 && R.n <= 64 &&
+         !ln_fusable(wdtype, R.n, hid) && gemm_kslices(N, R.n, K / 64) > 1;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {

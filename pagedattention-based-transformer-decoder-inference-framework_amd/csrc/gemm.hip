@@ -571,9 +571,43 @@ namespace {
 // k-steps per wave) is kept for the tuning entry.
 inline int pick_waves(const GemmArgs&, int) { return 8; }
 
+// Decode rows 17..32 (C4's 32 beams): 16-row workgroups (each row block
+// streams the weights; the repeat reads come from L2 / the Infinity Cache),
+// 4-wave workgroups for K < 4096, in place of 32-row tiles and split-K.
+// Graph-replayed sweep of every (NT, waves, rows) form (scripts/tune_gemm.py
+// --M 32, two runs agree within 0.1 us): qkv 7.0 -> 6.5 us, o_proj 4.8 ->
+// 3.6, fc2 10.1 -> 7.0 (fc1 keeps NT 2 x 32 rows, 7.8).  In the C4 step
+// (same box, scripts/gpu_lib_ab.sh) +3.3..4.1 % over split-K.  At 64 rows
+// (C3) the same forms lost 0.3 % to split-K, which stays there.
+struct TileChoice {
+  int nt, waves, mrows;
+};
+inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
+  if (a.ln_x || a.partial || a.M <= 16 || a.M > 32) return false;
+  const int ntiles = (a.N + 15) / 16;
+  const int K = a.KS * kstep;
+  if (ntiles < 384) {
+    t = K >= 4096 ? TileChoice{1, 8, 16} : TileChoice{1, 4, 16};
+    return true;
+  }
+  if (ntiles < 512) {
+    t = TileChoice{1, 4, 16};
+    return true;
+  }
+  return false;
+}
+
 template <GemmKind KIND>
 hipError_t launch_gemm(const GemmArgs& a, hipStream_t st, int nt_override = 0,
                        int waves_override = 0, int mrows_override = 0) {
+  TileChoice tc{0, 0, 0};
+  const bool narrow = nt_override == 0 && waves_override == 0 && mrows_override == 0 &&
+                      narrow_decode_tile(a, GemmTraits<KIND>::KSTEP, tc);
+  if (narrow) {
+    nt_override = tc.nt;
+    waves_override = tc.waves;
+    mrows_override = tc.mrows;
+  }
   const int NT = nt_override > 0 ? nt_override : pick_nt(a.N, a.M);
   const int waves = waves_override > 0 ? waves_override : pick_waves(a, NT);
   // rows per workgroup: 32 when the column grid alone cannot fill the CUs

@@ -1601,26 +1601,29 @@ extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,
 extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q, float* out,
                               const int32_t* context_lens, int B, int H, int T, int pps,
                               void* workspace, size_t workspace_bytes, void* stream) {
-  LLM_REQUIRE(kv && kv->head_dim == 128 && kv->page_size == 16 && H == kv->num_heads,
-              "pa_decode_tune: D=128, page 16 only");
+  LLM_REQUIRE(kv && (kv->head_dim == 128 || kv->head_dim == 64) && kv->page_size == 16 &&
+                  H == kv->num_heads,
+              "pa_decode_tune: D 128 (variants 0-13) or 64 (20-25), page 16 only");
+  const int D = kv->head_dim;
+  LLM_REQUIRE((D == 128) == (variant < 20), "pa_decode_tune: variant / head_dim mismatch");
   const int ntiles_max = std::max(1, (T + 15) / 16);
   pps = std::min(std::max(pps, 1), kMaxPps);
   const int nsplit = (ntiles_max + pps - 1) / pps;
   LLM_REQUIRE(nsplit > 1 && nsplit <= kMaxSplits, "pa_decode_tune: needs 2..128 splits");
-  const size_t need = (size_t)B * H * nsplit * (128 + 2) * sizeof(float);
+  const size_t need = (size_t)B * H * nsplit * (D + 2) * sizeof(float);
   LLM_REQUIRE(workspace && workspace_bytes >= need, "pa_decode_tune: workspace");
   PaSplitArgs a{};
   a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
   a.v_pool = static_cast<const uint8_t*>(kv->v_pool);
   a.page_table = kv->page_table;
-  a.q = q; a.q_stride = H * 128; a.out = out;
+  a.q = q; a.q_stride = H * D; a.out = out;
   a.context_lens = context_lens;
   a.B = B; a.H = H; a.T = T;
   a.num_pages = kv->num_pages; a.num_beams = kv->num_beams; a.max_tiles = kv->max_tiles;
   a.page_stride = kv_view_page_stride(*kv);
   a.pps = pps; a.nsplit = nsplit; a.group = 1; a.qscale = kLog2e;
   a.part_acc = static_cast<float*>(workspace);
-  a.part_ml = a.part_acc + (size_t)B * H * nsplit * 128;
+  a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   hipStream_t st = as_stream(stream);
   const dim3 grid((B * H * nsplit + 3) / 4), block(256);
   switch (variant) {  // NOLINT
@@ -1639,10 +1642,18 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
     case 12: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 2, 2, 0, true>), grid, block, 0, st, a); break;
     // 13: variant 1 without the full-page fast path (every token takes the validity selects)
     case 13: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 2, 0, false, false, LLM_F16, false>), grid, block, 0, st, a); break;
+    // D = 64 (C2): 20 production, 21 one 16 KiB stage, 22 8 KiB stages, 23 one
+    // 32 KiB stage, 24 / 25 loads only (16 KiB x 2, 32 KiB x 1)
+    case 20: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 16384, 2, 2>), grid, block, 0, st, a); break;
+    case 21: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 16384, 2, 1>), grid, block, 0, st, a); break;
+    case 22: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 8192, 2, 2>), grid, block, 0, st, a); break;
+    case 23: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 32768, 2, 1>), grid, block, 0, st, a); break;
+    case 24: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 16384, 2, 2, 0, true>), grid, block, 0, st, a); break;
+    case 25: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 32768, 2, 1, 0, true>), grid, block, 0, st, a); break;
     default: return fail(LLM_ERR_INVALID, "pa_decode_tune: variant");
   }
   LLM_HIP_RET(hipGetLastError());
-  PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, 128, T, 16, pps, nsplit,
+  PaMergeArgs mg{a.part_acc, a.part_ml, out, context_lens, B, H, D, T, 16, pps, nsplit,
                  kv->max_tiles};
   hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
   LLM_HIP_RET(hipGetLastError());

@@ -42,8 +42,9 @@ for name, K, N in shapes:
     Ap = llm_capi.pack_weights(A.t().contiguous(), llm_capi.LLM_I8)  # A-fragment order
     llm_capi.check(lib.i8_gemm_tune(1, 8, 0, 0, A.data_ptr(), K, Wp.data_ptr(),
                                     ref.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(), None))
-    for nt, ks, apk, mr in [(1, 8, 1, 64), (2, 8, 1, 64), (1, 8, 1, 32), (2, 8, 1, 32),
-                            (1, 8, 1, 16), (2, 4, 1, 64), (1, 4, 1, 32), (1, 4, 1, 16)]:
+    grid = [(nt, w, 1, mr) for nt in (1, 2) for w in (4, 8) for mr in (16, 32, 64)
+            if mr >= 16 * ((M + 63) // 64) or mr < M or mr == 16]
+    for nt, ks, apk, mr in grid:
         for _ in range(1):
             C.zero_()
             llm_capi.check(lib.i8_gemm_tune(nt, ks, mr, apk, (Ap if apk else A).data_ptr(), K,

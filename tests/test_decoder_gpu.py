@@ -617,17 +617,20 @@ def test_forced_step_48_rows(gpu, oracle):
     assert n_flips < 1e-3 * n_vals
 
 
-def test_forced_split_k_hidden_2048(gpu, oracle):
-    """hid 2048 at 16 rows: the LayerNorms are launches (the rows' fp32 image is
-    too big for the GEMM prologue), so o_proj and the non-final fc2 run
+@pytest.mark.parametrize("rows", [24, 48])
+def test_forced_split_k_hidden_2048(gpu, oracle, rows):
+    """hid 2048: the LayerNorms are launches (the rows' fp32 image is too big
+    for the GEMM prologue).  At 48 rows o_proj and the non-final fc2 run
     split-K (two k slices of exact int32 partials, summed with the GEMM's
-    epilogue by the next LayerNorm launch).  Teacher forced, north_star bar."""
+    epilogue by the next LayerNorm launch); at 24 rows the GEMMs take the
+    narrow 16-row tiles (two row blocks, 4-wave workgroups for K < 4096).
+    Teacher forced, north_star bar."""
     from oracle.oracle import OracleDecoder
     w = _int8_model(oracle, L=2, H=16, D=128, V=512, S=24, seed=41)
-    dec = _make_gpu_decoder(w, max_batch=16)
-    taps = _Taps(dec, w, 16)
+    dec = _make_gpu_decoder(w, max_batch=rows)
+    taps = _Taps(dec, w, rows)
     rng = np.random.default_rng(5)
-    prompts = [list(rng.integers(0, 512, 3)) for _ in range(16)]
-    _, worst, n_vals, n_flips = _forced_lockstep(dec, OracleDecoder(oracle, w, 16), taps, prompts,
-                                                 gen=4, V=512)
+    prompts = [list(rng.integers(0, 512, 3)) for _ in range(rows)]
+    _, worst, n_vals, n_flips = _forced_lockstep(dec, OracleDecoder(oracle, w, rows), taps,
+                                                 prompts, gen=4, V=512)
     assert n_flips < 1e-3 * n_vals, (n_flips, n_vals)
