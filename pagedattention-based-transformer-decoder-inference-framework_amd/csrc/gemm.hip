@@ -828,4 +828,18 @@ extern "C" int i8_gemm_tune(int nt, int waves, int mrows, int a_packed, const in
   hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream), nt, waves, mrows);
   return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune");
 }
+
+// The FP16 GEMM with a forced form (A in packed-A order when a_packed).
+extern "C" int f16_gemm_tune(int nt, int waves, int mrows, int a_packed, const void* A, int lda,
+                             const void* W_packed, float* C, int M, int N, int K, void* stream) {
+  GemmArgs a{};
+  a.a_packed = a_packed;
+  a.A = static_cast<const uint8_t*>(A);
+  a.lda = lda;
+  a.B = static_cast<const uint8_t*>(W_packed);
+  a.M = M; a.N = N; a.K = K; a.KS = K / 32;
+  a.C = C; a.c_cols = N; a.c_ld = N;
+  hipError_t e = launch_gemm<GemmKind::F16>(a, as_stream(stream), nt, waves, mrows);
+  return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "f16_gemm_tune");
+}
 #endif  // LLM_TUNING
