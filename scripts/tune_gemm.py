@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--M", type=int, default=64)
 ap.add_argument("--reps", type=int, default=50)
 ap.add_argument("--hid", type=int, default=2048)
+ap.add_argument("--copies", type=int, default=8)
 args = ap.parse_args()
 lib = llm_capi.load_tune()  # tuning build: `make tune`
 lib.i8_gemm_tune.restype = ctypes.c_int
@@ -33,7 +34,8 @@ for name, K, N in shapes:
     W = torch.randint(-128, 128, (K, N), dtype=torch.int8, device="cuda")
     Wp = llm_capi.pack_weights(W, llm_capi.LLM_I8)
     # distinct weight copies so consecutive launches stream from HBM, not L2/MALL
-    copies = [Wp.clone() for _ in range(8)]
+    # (--copies 64: past the 256 MB Infinity Cache, as in the decode step)
+    copies = [Wp.clone() for _ in range(args.copies)]
     A = torch.randint(-128, 128, (M, K), dtype=torch.int8, device="cuda")
     sa = torch.rand(M, device="cuda")
     sw = torch.rand(N, device="cuda")
@@ -58,7 +60,7 @@ for name, K, N in shapes:
             st = torch.cuda.current_stream().cuda_stream
             for r in range(args.reps):
                 lib.i8_gemm_tune(nt, ks, mr, apk, (Ap if apk else A).data_ptr(), K,
-                                 copies[r % 8].data_ptr(),
+                                 copies[r % len(copies)].data_ptr(),
                                  C.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(),
                                  ctypes.c_void_p(st))
         g.replay()
