@@ -1078,12 +1078,22 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   }
   __syncthreads();
   float am = 0.f;
-  for (int i = threadIdx.x; i < hid; i += blockDim.x) {
-    const float v = row[i];
-    am = fmaxf(am, fabsf(v));
-    if (a.out) a.out[(size_t)b * hid + i] = v;
-    if (a.out16)
-      a.out16[a.pack ? a_frag_off_f16(b, i, hid >> 5) : (size_t)b * hid + i] = (_Float16)v;
+  // packed int8 o_proj input only (the decode step): 4 values per thread, one
+  // dword store each (4 consecutive k are 4 consecutive bytes of a fragment)
+  const bool quad = a.q && a.pack && !a.out && !a.out16 && hid % 64 == 0;
+  if (quad) {
+    for (int i4 = threadIdx.x; i4 < hid / 4; i4 += blockDim.x) {
+      const f32x4 v = reinterpret_cast<const f32x4*>(row)[i4];
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+  } else {
+    for (int i = threadIdx.x; i < hid; i += blockDim.x) {
+      const float v = row[i];
+      am = fmaxf(am, fabsf(v));
+      if (a.out) a.out[(size_t)b * hid + i] = v;
+      if (a.out16)
+        a.out16[a.pack ? a_frag_off_f16(b, i, hid >> 5) : (size_t)b * hid + i] = (_Float16)v;
+    }
   }
   if (!a.q) return;
   am = ln_wave_max(am);  // DPP (wave_max shuffles through LDS)
@@ -1092,10 +1102,16 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   am = sh[0];
   for (int i = 1; i < nw; ++i) am = fmaxf(am, sh[i]);
   const float scale = 127.f / (am + 1e-6f);
-  for (int i = threadIdx.x; i < hid; i += blockDim.x) {
-    float y = roundf(__fmul_rn(row[i], scale));
-    y = fminf(fmaxf(y, -128.f), 127.f);
-    a.q[a.pack ? a_frag_off_i8(b, i, hid >> 6) : (size_t)b * hid + i] = (int8_t)(int)y;
+  if (quad) {
+    for (int i4 = threadIdx.x; i4 < hid / 4; i4 += blockDim.x)
+      *reinterpret_cast<uint32_t*>(a.q + a_frag_off_i8(b, 4 * i4, hid >> 6)) =
+          ln_quant4(reinterpret_cast<const f32x4*>(row)[i4], scale);
+  } else {
+    for (int i = threadIdx.x; i < hid; i += blockDim.x) {
+      float y = roundf(__fmul_rn(row[i], scale));
+      y = fminf(fmaxf(y, -128.f), 127.f);
+      a.q[a.pack ? a_frag_off_i8(b, i, hid >> 6) : (size_t)b * hid + i] = (int8_t)(int)y;
+    }
   }
   if (threadIdx.x == 0) a.inv_scale[b] = 1.0f / scale;
 }
