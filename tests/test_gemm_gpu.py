@@ -22,6 +22,8 @@ def _dev(a):
     (130, 512, 256), (64, 256, 16), (5, 64, 32),
     # prefill-chunk row counts (M up to 512)
     (512, 2048, 2048), (300, 512, 256), (256, 8192, 512), (513, 1024, 96),
+    # 17..32 rows: the 16-row tile forms (narrow_decode_tile), every output class
+    (17, 2048, 2048), (24, 2048, 6144), (32, 8192, 2048), (32, 2048, 8192), (20, 768, 768),
 ])
 def test_i8_gemm_exact(gpu, oracle, M, K, N):
     import llm_capi
