@@ -245,6 +245,9 @@ def main():
     ap.add_argument("--gather", default="logits", choices=["logits", "ids"],
                     help="N > 1: what each step gathers to rank 0 (SURVEY §8e)")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--contiguous-pages", action="store_true",
+                    help="sensitivity runs only: pages in allocation order instead of the "
+                         "shuffled pool SURVEY §8d measures on")
     args = ap.parse_args()
 
     import torch
@@ -286,9 +289,9 @@ def main():
     del w
     if "beams" in cfg:
         dec.begin_beams(cfg["seqs"], cfg["beams"], cfg["shared"], T - cfg["shared"],
-                        args.seed + rank, True)
+                        args.seed + rank, not args.contiguous_pages)
     else:
-        dec.begin_synthetic(B, T, args.seed + rank, True)
+        dec.begin_synthetic(B, T, args.seed + rank, not args.contiguous_pages)
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s")
 
     # the multi-rank decode loop (dist_decode.ShardedDecode / timed_run): each
@@ -354,7 +357,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int8 GEMM (i32 acc) + fp16 KV attention (fp32 acc)"
             if cfg["cls"] == "INT8Decoder" else "fp16 GEMM + fp16 KV attention (fp32 acc)",
-            "data": "synthetic (random-init weights, random fp16 KV context, shuffled pages)",
+            "data": "synthetic (random-init weights, random fp16 KV context, "
+                    + ("pages in allocation order)" if args.contiguous_pages else "shuffled pages)"),
             "config": {"workload": cfg["workload"] + (f"; strong scaling: {args.global_batch} rows "
                                                       f"over {world} GPU(s)" if strong else ""),
                        "global_batch": args.global_batch if strong else B * world,
