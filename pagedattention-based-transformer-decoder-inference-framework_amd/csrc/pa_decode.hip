@@ -69,7 +69,16 @@ struct PaSplitArgs {
   float qscale;
   int balance16;  // BEAM, dynamic splits: cost of a beam-private tile in 1/16ths of a
                   // shared tile (>= 16) for cost-balanced split boundaries; 0: off
+  // WGM (workgroup merge): one workgroup of nsplit (<= 8) waves per (b, h); the
+  // splits meet in LDS and wave 0 writes the merged head straight into the
+  // o_proj input, no merge launch.  out16: fp16 [B][H*D] (packed-A order when
+  // pack), out (if set): fp32 [B][H*D]
+  _Float16* out16;
+  int pack;
+  int wgm;
 };
+
+constexpr int kWgmMaxSplits = 8;  // one merge batch (pa_merge_row_kernel's kMergeBatch)
 
 constexpr int kMaxPps = 128;     // page ids held in two registers per lane
 constexpr int kMaxSplits = 128;  // split weights held in two registers per merge lane
@@ -132,10 +141,13 @@ constexpr int kKvLoadAux = 2;
 // the next chunk's quarter in flight during the current chunk's math) and
 // every wave runs its own softmax/AV over the full chunk from LDS.  The rest
 // of the split (beam-private pages) takes the per-wave direct path.
+// WGM: the workgroup-merge form (PaSplitArgs::wgm): blockDim = 64 * nsplit,
+// one workgroup per (b, h), wave w = split w.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
-          int KVT = LLM_F16, bool FULLPATH = true>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
+          int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false>
+__global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
+__attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
   constexpr int ES = kv_elem_bytes<KVT>();
   constexpr int EPL = 16 / ES;  // elements per lane per 16-byte load
@@ -147,9 +159,10 @@ void pa_split_kernel(PaSplitArgs a) {
   constexpr int NR = U * NI;
   static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1, "bad D/TS");
 
+  static_assert(!(WGM && (DIRECT || BEAM)), "the workgroup merge is a split form");
   const int lane = lane_id();
-  const int wid = blockIdx.x * 4 + wave_id_uniform();
-  const int G = BEAM ? 4 : a.group;
+  const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
+  const int G = BEAM ? 4 : WGM ? 1 : a.group;
   const int gi = wid % G;  // row within the group (fastest: adjacent waves)
   const int rest = wid / G;
   const int s = rest % a.nsplit;
@@ -263,7 +276,8 @@ void pa_split_kernel(PaSplitArgs a) {
         for (int e = 0; e < EPL; e += 4) *reinterpret_cast<f32x4*>(o + e) = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    return;
+    if constexpr (!WGM) return;
+    count = 0;  // WGM: no partial (the merge reads splits < ns only), but meet the workgroup
   }
 
   // Page ids of this split: lane j holds pages j and 64 + j
@@ -481,6 +495,79 @@ void pa_split_kernel(PaSplitArgs a) {
       acc[e] = acc[e] * ca + ao * cb;
     }
     m = mn;
+  }
+
+  if constexpr (WGM) {
+    // The workgroup's waves are the splits of one (b, h): their states meet in
+    // LDS and wave 0 merges them with pa_merge_row_kernel's arithmetic (same
+    // weights, same sequential order over splits 0..7, zero weights past ns),
+    // so the o_proj input is bit-identical to the split + merge launches'.
+    __shared__ float wg_ml[kWgmMaxSplits][2];
+    __shared__ __attribute__((aligned(16))) float wg_acc[kWgmMaxSplits][D];
+    if (lane < LPT) {
+#pragma unroll
+      for (int e = 0; e < EPL; e += 4)
+        *reinterpret_cast<f32x4*>(&wg_acc[s][c * EPL + e]) =
+            f32x4{acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+    }
+    if (lane == 0) {
+      wg_ml[s][0] = m;
+      wg_ml[s][1] = l;
+    }
+    __syncthreads();
+    if (s != 0) return;
+    const int pps = row_pps(a.pps, a.nsplit, ntiles);
+    const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
+    const float m0 = lane < ns ? wg_ml[lane][0] : kNegSentinel;
+    const float l0 = lane < ns ? wg_ml[lane][1] : 0.f;
+    const float M = ln_wave_max(fmaxf(m0, kNegSentinel));
+    float o[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) o[e] = 0.f;
+    if (ns > 0 && M > 0.5f * kNegSentinel) {
+      const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
+      float L = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < kWgmMaxSplits; ++s2)
+        if (s2 < ns) {
+          const float ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l0), s2));
+          const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
+          L += ls * ws;
+        }
+      const float inv = 1.0f / (L + 1e-6f);
+      float am[EPL];
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) am[e] = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < kWgmMaxSplits; ++s2) {
+        const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));  // 0 past ns
+        const float* src = &wg_acc[min(s2, max(ns - 1, 0))][c * EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) am[e] += src[e] * ws;
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) o[e] = am[e] * inv;
+    }
+    if (lane < LPT) {
+      const int hid = a.H * D;
+      const int k0 = h * D + c * EPL;
+      if (a.out) {
+        float* op = a.out + (size_t)b * hid + k0;
+#pragma unroll
+        for (int e = 0; e < EPL; e += 4) *reinterpret_cast<f32x4*>(op + e) = f32x4{o[e], o[e + 1], o[e + 2], o[e + 3]};
+      }
+      if (a.out16) {
+        static_assert(KVT != LLM_F16 || EPL == 8, "fp16 lanes hold 8 dims: one 16-byte store");
+        if constexpr (EPL == 8) {
+          f16x8 pk;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pk[e] = (_Float16)o[e];
+          *reinterpret_cast<f16x8*>(a.out16 + (a.pack ? a_frag_off_f16(b, k0, hid >> 5)
+                                                      : (size_t)b * hid + k0)) = pk;
+        }
+      }
+    }
+    return;
   }
 
   if (lane < LPT) {
@@ -1161,6 +1248,15 @@ bool beam_mfma_on() {
   return false;
 #endif
 }
+// Workgroup-merge form of the fp16 row-output launch (PaSplitArgs::wgm); the
+// tuning build's LLM_WG_MERGE=0 restores split + merge launches (A/B, parity).
+bool wg_merge_on() {
+#if LLM_TUNING
+  return env_int("LLM_WG_MERGE", 1) != 0;  // read per launch: a test flips it in-process
+#else
+  return true;
+#endif
+}
 int beam_mfma_balance16() {
 #if LLM_TUNING
   static const int v = env_int("LLM_BEAM_MFMA_BALANCE16", 64);
@@ -1191,6 +1287,12 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
     return hipGetLastError();
   }
   constexpr int ST = split_stages<D, TS, LLM_F16>();
+  if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct, not lean
+    hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
+                                        LLM_F16, true, true>),
+                       dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.group == 4 && !direct && !lean && ST == 2) {
     // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
     // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
@@ -1528,7 +1630,15 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // (4 waves per SIMD against the plain kernel's 2: C4 8 splits, not 4)
   if (pps_fixed <= 0 && !lean && row_group == 4 && kv->kv_dtype == LLM_F16)
     resident = std::max(resident, beam_resident_waves_for(D, TS));
-  const int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
+  int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
+#if LLM_TUNING
+  // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
+  // eligible launches (fp16 row outputs, dynamic splits)
+  if (rows && rows->out16 && !rows->q && row_group == 1 && pps_fixed <= 0 && !lean) {
+    const int f = env_int("LLM_WGM_SPLITS", 0);
+    if (f >= 2 && f <= kWgmMaxSplits && (long long)f * kMaxPps >= ntiles_max) nsplit = f;
+  }
+#endif
   if (nsplit > kMaxSplits || (long long)nsplit * (pps_fixed > 0 ? pps_fixed : kMaxPps) < ntiles_max)
     return fail(LLM_ERR_UNSUPPORTED,
                 "pa_decode: at most 128 splits of at most 128 pages per row (raise "
@@ -1564,6 +1674,17 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   }
   a.balance16 = beam_balance16();
+  // fp16 o_proj input only (the FP16 decoder's attention): with at most one
+  // merge batch of splits per (b, h) the splits merge inside the split
+  // launch's workgroup (C2: 12 merge launches per step fewer)
+  const bool wgm = row_out && !direct && rows->out16 && !rows->q && a.group == 1 && !lean &&
+                   nsplit <= kWgmMaxSplits && kv->kv_dtype == LLM_F16 && wg_merge_on();
+  if (wgm) {
+    a.wgm = 1;
+    a.out16 = static_cast<_Float16*>(rows->out16);
+    a.pack = rows->pack;
+    a.out = rows->keep_out ? out : nullptr;
+  }
   hipError_t e;
   bool beam = false;  // the beam kernel ran: every split holds a partial
   switch (D) {
@@ -1573,6 +1694,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
+  if (wgm) return LLM_OK;
   if (row_out && !direct)
     return pa_merge_rows_internal(a.part_acc, a.part_ml, rows->keep_out ? out : nullptr, rows,
                                   context_lens, -1, B, H, D, T, TS, beam ? -1 : pps_fixed, nsplit,

@@ -360,20 +360,22 @@ def _f16_reference_logits(w, tokens_per_step, oracle):
     return all_logits
 
 
-@pytest.mark.parametrize("H", [2, 12])
-def test_cuda_decoder_fp16_vs_oracle(gpu, oracle, H):
+@pytest.mark.parametrize("H,S", [(2, 40), (12, 40), (12, 512)])
+def test_cuda_decoder_fp16_vs_oracle(gpu, oracle, H, S):
     """CUDADecoder (fp16 weights, fp16 GEMM inputs, fp16 KV) against the
     oracle's restated CUDADecoder step (oracle.cpp f16_gemm path), 24 steps of
     ragged prompts then fed-back tokens: logits within LOGIT_TOL, tokens exact
     unless the oracle's top two are within TIE_TOL.  No int8 rounding here, so
     no teacher forcing is needed (an fp16 rounding flip moves a logit ~1e-6).
     A float64 numpy restatement (_f16_reference_logits) agrees as well.
-    H 12 is C2's width (hid 768, inter 3072)."""
+    H 12 is C2's width (hid 768, inter 3072).  S 512 gives the attention 4
+    splits, so it runs in the workgroup-merge form (splits past a short row's
+    tiles empty); S 40 is a single-split launch."""
     torch = _torch()
     import llm_decoder
     from oracle.oracle import OracleDecoder
     rng = np.random.default_rng(9)
-    L, D, V, S = 2, 64, 300, 40
+    L, D, V = 2, 64, 300
     w = _f16_model(rng, L, H, D, V, S)
     c = w["cfg"]
     dec = llm_decoder.CUDADecoder(L, H, D, c["hid"], V, S, max_batch=2)

@@ -1,0 +1,100 @@
+"""Workgroup-merge form of the FP16 decoder's attention (pa_decode.hip WGM).
+
+When the split count of a row-output launch is 2..8, the splits of one
+(row, head) run as the waves of one workgroup and merge in LDS, replacing the
+pa_merge_row_kernel launch.  The merge repeats that kernel's arithmetic, so a
+decoder step must produce the SAME BITS either way.  The tuning build's
+LLM_WG_MERGE=0 restores split + merge launches; both forms are stepped through
+the C-ABI (llm_decoder_create / set_f16_weights / begin_synthetic / step) at
+C2's width (12 heads x 64, 16 rows), at a long context (every split full) and
+a short one (splits past the row's tiles are empty: ns < nsplit).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class _Cfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("num_layers", "num_heads", "head_dim", "hidden_dim",
+                                            "vocab_size", "max_seq_len", "inter_dim", "page_size",
+                                            "weight_dtype", "max_batch")] + [
+        ("attn_scale", ctypes.c_float), ("num_pages", ctypes.c_longlong)]
+
+
+class _F16W(ctypes.Structure):
+    _fields_ = [("emb", ctypes.c_void_p)] + [(n, ctypes.c_void_p) for n in (
+        "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wqkv", "wo", "w1", "w2", "b1", "b2")]
+
+
+def _model(rng, L, H, D, V):
+    hid, inter = H * D, 4 * H * D
+    w = {"emb": rng.standard_normal((V, hid)).astype(np.float16)}
+    for k in ("ln1_g", "ln2_g"):
+        w[k] = (1 + 0.1 * rng.standard_normal((L, hid))).astype(np.float32)
+    for k in ("ln1_b", "ln2_b"):
+        w[k] = (0.1 * rng.standard_normal((L, hid))).astype(np.float32)
+    w["wqkv"] = (0.02 * rng.standard_normal((L, hid, 3 * hid))).astype(np.float16)
+    w["wo"] = (0.02 * rng.standard_normal((L, hid, hid))).astype(np.float16)
+    w["w1"] = (0.02 * rng.standard_normal((L, hid, inter))).astype(np.float16)
+    w["w2"] = (0.02 * rng.standard_normal((L, inter, hid))).astype(np.float16)
+    w["b1"] = (0.02 * rng.standard_normal((L, inter))).astype(np.float32)
+    w["b2"] = (0.02 * rng.standard_normal((L, hid))).astype(np.float32)
+    return {k: np.ascontiguousarray(v) for k, v in w.items()}
+
+
+def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm):
+    """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`."""
+    import torch
+    import llm_capi
+    os.environ["LLM_WG_MERGE"] = "1" if wgm else "0"
+    lib.llm_decoder_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_void_p)]
+    lib.llm_decoder_set_f16_weights.argtypes = [ctypes.c_void_p, ctypes.POINTER(_F16W)]
+    lib.llm_decoder_begin_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_uint64, ctypes.c_int]
+    lib.llm_decoder_step.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+    lib.llm_decoder_sync.argtypes = [ctypes.c_void_p]
+    lib.llm_decoder_destroy.argtypes = [ctypes.c_void_p]
+    lib.llm_decoder_destroy.restype = None
+    cfg = _Cfg(L, H, D, H * D, V, S, 0, 16, llm_capi.LLM_F16, B, 1.0, 0)
+    dec = ctypes.c_void_p()
+    llm_capi.check(lib.llm_decoder_create(ctypes.byref(cfg), ctypes.byref(dec)), lib)
+    try:
+        ww = _F16W(*[w[k].ctypes.data for k in ("emb", "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wqkv",
+                                                 "wo", "w1", "w2", "b1", "b2")])
+        llm_capi.check(lib.llm_decoder_set_f16_weights(dec, ctypes.byref(ww)), lib)
+        llm_capi.check(lib.llm_decoder_begin_synthetic(dec, B, ctx, 77, 1), lib)
+        rng = np.random.default_rng(5)
+        out = []
+        logits = torch.empty((B, V), device="cuda")
+        for _ in range(steps):
+            tok = rng.integers(0, V, B).astype(np.int32)
+            llm_capi.check(lib.llm_decoder_step(dec, tok.ctypes.data, logits.data_ptr(), None, None),
+                           lib)
+            llm_capi.check(lib.llm_decoder_sync(dec), lib)
+            out.append(logits.cpu().numpy().copy())
+        return np.stack(out)
+    finally:
+        lib.llm_decoder_destroy(dec)
+        os.environ.pop("LLM_WG_MERGE", None)
+
+
+@pytest.mark.parametrize("ctx", [1500, 40])
+def test_wg_merge_bitwise_c2_width(gpu, ctx):
+    import llm_capi
+    tune = llm_capi.load_tune()
+    L, H, D, V, S, B = 2, 12, 64, 512, 2100, 16
+    # the launch takes the workgroup-merge form only for 2..8 splits
+    ns = -(-((S + 15) // 16) // llm_capi.load().pa_decode_pages_per_split(B, H, S, 16, (S + 15) // 16))
+    assert 2 <= ns <= 8, ns
+    w = _model(np.random.default_rng(3), L, H, D, V)
+    on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True)
+    off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False)
+    assert np.isfinite(on).all()
+    assert np.array_equal(on.view(np.uint32), off.view(np.uint32)), np.abs(on - off).max()
+    prod = _run(llm_capi.load(), w, L, H, D, V, S, B, ctx, 3, True)
+    assert np.array_equal(prod.view(np.uint32), on.view(np.uint32))
