@@ -1402,7 +1402,13 @@ long long max_nsplit(int B, int H, int ntiles) {
 // 1 x 16 x 8192: 32.8 -> 26.4 us; 4 x 12 x 1024 unchanged (9.9 us).
 constexpr int kShortPps = 32;
 constexpr long long kMinLaunchWaves = 512;
-int choose_nsplit(int B, int H, int ntiles, int pps_fixed, long long resident) {
+// Workgroup-merge launches (PaSplitArgs::wgm) have no merge launch to feed, so
+// their splits stay long: C2 (130 tiles) 3 splits, not 5.  Same-box C2 sweep
+// (scripts/gpu_wgm_splits.sh, forced splits 2 / 3 / 4 / 5 / 6 / 8):
+// 27.4-28.0k / 29.6-30.1k / 29.1-29.2k / 28.4k / 28.6-28.9k / 28.2-29.0k tok/s.
+constexpr int kWgmShortPps = 64;
+int choose_nsplit(int B, int H, int ntiles, int pps_fixed, long long resident,
+                  int short_pps = kShortPps) {
   ntiles = std::max(ntiles, 1);
   if (pps_fixed > 0) {
     const int pps = std::min(pps_fixed, kMaxPps);
@@ -1416,8 +1422,8 @@ int choose_nsplit(int B, int H, int ntiles, int pps_fixed, long long resident) {
     if (cand >= lo) { ns = cand; break; }
   }
   ns = std::min<long long>(ns, std::max(1, (ntiles + kMinPps - 1) / kMinPps));
-  if ((ntiles + ns - 1) / ns < kShortPps)
-    ns = std::min(ns, std::max<long long>((ntiles + kShortPps - 1) / kShortPps,
+  if ((ntiles + ns - 1) / ns < short_pps)
+    ns = std::min(ns, std::max<long long>((ntiles + short_pps - 1) / short_pps,
                                           (kMinLaunchWaves + bh - 1) / bh));
   ns = std::max(ns, lo);
   return (int)std::min(ns, max_nsplit(B, H, ntiles));
@@ -1630,7 +1636,16 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // (4 waves per SIMD against the plain kernel's 2: C4 8 splits, not 4)
   if (pps_fixed <= 0 && !lean && row_group == 4 && kv->kv_dtype == LLM_F16)
     resident = std::max(resident, beam_resident_waves_for(D, TS));
+  // fp16 o_proj input only (the FP16 decoder's attention): with at most one
+  // merge batch of splits per (b, h) the splits merge inside the split
+  // launch's workgroup (C2: 12 merge launches per step fewer), with long splits
+  const bool wgm_ok = row_out && rows->out16 && !rows->q && row_group == 1 && !lean &&
+                      kv->kv_dtype == LLM_F16 && wg_merge_on();
   int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
+  if (wgm_ok && pps_fixed <= 0) {
+    const int nw = choose_nsplit(B, H, ntiles_max, 0, resident, kWgmShortPps);
+    if (nw >= 2 && nw <= kWgmMaxSplits) nsplit = nw;
+  }
 #if LLM_TUNING
   // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
   // eligible launches (fp16 row outputs, dynamic splits)
@@ -1674,11 +1689,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   }
   a.balance16 = beam_balance16();
-  // fp16 o_proj input only (the FP16 decoder's attention): with at most one
-  // merge batch of splits per (b, h) the splits merge inside the split
-  // launch's workgroup (C2: 12 merge launches per step fewer)
-  const bool wgm = row_out && !direct && rows->out16 && !rows->q && a.group == 1 && !lean &&
-                   nsplit <= kWgmMaxSplits && kv->kv_dtype == LLM_F16 && wg_merge_on();
+  const bool wgm = wgm_ok && !direct && a.group == 1 && nsplit <= kWgmMaxSplits;
   if (wgm) {
     a.wgm = 1;
     a.out16 = static_cast<_Float16*>(rows->out16);

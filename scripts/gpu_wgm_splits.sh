@@ -13,6 +13,6 @@ run() {  # name, LD path, env...
 }
 for r in 1 2; do
   run auto.$r "" X=1 || exit 1
-  for s in 3 4 6 8; do run s$s.$r $R/ab_old LLM_WGM_SPLITS=$s || exit 1; done
+  for s in ${SPLITS:-3 4 6 8}; do run s$s.$r $R/ab_old LLM_WGM_SPLITS=$s || exit 1; done
   run merge.$r $R/ab_old LLM_WG_MERGE=0 || exit 1
 done

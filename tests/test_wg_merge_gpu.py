@@ -46,11 +46,13 @@ def _model(rng, L, H, D, V):
     return {k: np.ascontiguousarray(v) for k, v in w.items()}
 
 
-def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm):
-    """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`."""
+def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0):
+    """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`
+    (tuning build: splits > 0 forces the split count)."""
     import torch
     import llm_capi
     os.environ["LLM_WG_MERGE"] = "1" if wgm else "0"
+    os.environ["LLM_WGM_SPLITS"] = str(splits)
     lib.llm_decoder_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_void_p)]
     lib.llm_decoder_set_f16_weights.argtypes = [ctypes.c_void_p, ctypes.POINTER(_F16W)]
     lib.llm_decoder_begin_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -81,20 +83,23 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm):
     finally:
         lib.llm_decoder_destroy(dec)
         os.environ.pop("LLM_WG_MERGE", None)
+        os.environ.pop("LLM_WGM_SPLITS", None)
 
 
 @pytest.mark.parametrize("ctx", [1500, 40])
 def test_wg_merge_bitwise_c2_width(gpu, ctx):
+    """Same split count, with and without the workgroup merge: same bits (at
+    ctx 40 = 3 tiles, 5 splits leave two empty); and the product build's own
+    split choice equals the tuning build's."""
     import llm_capi
     tune = llm_capi.load_tune()
     L, H, D, V, S, B = 2, 12, 64, 512, 2100, 16
-    # the launch takes the workgroup-merge form only for 2..8 splits
-    ns = -(-((S + 15) // 16) // llm_capi.load().pa_decode_pages_per_split(B, H, S, 16, (S + 15) // 16))
-    assert 2 <= ns <= 8, ns
     w = _model(np.random.default_rng(3), L, H, D, V)
-    on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True)
-    off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False)
-    assert np.isfinite(on).all()
-    assert np.array_equal(on.view(np.uint32), off.view(np.uint32)), np.abs(on - off).max()
+    for ns in (3, 5, 8):
+        on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, ns)
+        off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False, ns)
+        assert np.isfinite(on).all()
+        assert np.array_equal(on.view(np.uint32), off.view(np.uint32)), (ns, np.abs(on - off).max())
+    auto = _run(tune, w, L, H, D, V, S, B, ctx, 3, True)
     prod = _run(llm_capi.load(), w, L, H, D, V, S, B, ctx, 3, True)
-    assert np.array_equal(prod.view(np.uint32), on.view(np.uint32))
+    assert np.array_equal(prod.view(np.uint32), auto.view(np.uint32))
