@@ -130,10 +130,32 @@ def attention_launch_bytes(cfg, T, B, unique=False):
     return 2 * kv_tokens * H * D * 2 + B * H * nt * 4 + 2 * B * H * D * 4
 
 
-def time_attention(dec, cfg, B, T, max_seq, iters=20, row_group=1):
-    """Live HIP-event timing of the decoder's paged-attention launch (split +
-    merge, the same kernel instantiation and grid as inside the step graph) on
-    layer 0's pools, on torch's current stream."""
+def time_attention(dec, iters=20, row_group=None):
+    """Live HIP-event timing of the decoder's own paged-attention launch of
+    layer 0 (llm_decoder_run_attention: the step graph's kernels, grid and
+    outputs -- split + merge-and-quantise for INT8, the workgroup-merge form
+    for FP16, the beam-group schedule for beams), enqueued on torch's current
+    stream so the events bracket exactly those kernels."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        dec.run_attention(0, st)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def time_attention_plain(dec, cfg, B, T, max_seq, iters=20):
+    """The same attention as a plain pa_decode_grouped launch (row_group 1,
+    fp32 output; beam configs: the schedule without beam awareness)."""
     import torch
     import llm_decoder
     H, D = cfg["H"], cfg["D"]
@@ -148,7 +170,7 @@ def time_attention(dec, cfg, B, T, max_seq, iters=20, row_group=1):
     def run():
         llm_decoder.paged_attention(dec.kv_handle, 0, q.data_ptr(), out.data_ptr(), 0,
                                     ctx.data_ptr(), B, H, D, max_seq, 1.0, 0, 1.0,
-                                    ws.data_ptr(), wsb, st, row_group)
+                                    ws.data_ptr(), wsb, st, 1)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -161,7 +183,47 @@ def time_attention(dec, cfg, B, T, max_seq, iters=20, row_group=1):
     return s.elapsed_time(e) / iters * 1e-3
 
 
-def cpu_baseline(cfg, budget_s=20.0):
+FORM_NAMES = {0: "direct (one split)", 1: "split + pa_merge_kernel",
+              2: "split + pa_merge_row_kernel (merge + per-row int8 quantisation)",
+              3: "split with workgroup merge (packed fp16 o_proj input)"}
+
+
+def cpu_threads():
+    """Threads of the CPU baseline: the job's OpenMP share (OMP_NUM_THREADS:
+    the GPU pool gives each 1-GPU job 16 of the host's CPUs and sets it so;
+    BASELINE.md's $(nproc) would take every CPU of a host shared by 8 GPUs'
+    jobs), else every CPU this process may run on."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    n = int(env) if env.isdigit() and int(env) > 0 else avail
+    return min(n, avail), avail
+
+
+def cpu_baseline(cfg_name, budget_s=20.0):
+    """The CPU baseline, run in a child process (no GPU in it) whose OpenMP
+    runtime starts with OMP_PROC_BIND=close, OMP_PLACES=cores and
+    OMP_NUM_THREADS = cpu_threads(): those are read when
+    the OpenMP runtime starts, which in this process torch has already done."""
+    import subprocess
+    threads, avail = cpu_threads()
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close",
+               OMP_PLACES="cores")
+    r = subprocess.run([sys.executable, str(Path(__file__).resolve()), "--cpu-baseline-child",
+                        "--config", cfg_name, "--cpu-budget", str(budget_s)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed ({r.returncode}): {r.stderr[-2000:]}")
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    res["cpus_available"] = avail
+    res["cpu"]["cpus_available"] = avail  # (the child's own affinity is one place once bound)
+    res["omp"] = {"OMP_NUM_THREADS": threads, "OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}
+    return res
+
+
+def cpu_baseline_run(cfg, budget_s=20.0):
     """The oracle (restated INT8Decoder / CUDADecoder, C++/OpenMP, built with
     -march=native on this host) timed on this host's cores over a bounded
     sample of the same workload.  C1 (the reference's own CPU-runnable
@@ -171,6 +233,9 @@ def cpu_baseline(cfg, budget_s=20.0):
     from oracle.oracle import Oracle, OracleDecoder, host_cpu, native_build
     native = native_build()
     o = Oracle(bench="native" if native else True)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if threads > 0:
+        o.lib.oracle_set_num_threads(threads)
     L, H, D, V, T, B = cfg["L"], cfg["H"], cfg["D"], cfg["V"], cfg["T"], cfg["B"]
     hid = H * D
     full = cfg.get("cpu_full", False)
@@ -238,6 +303,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: this many rows in total, sharded over the ranks "
@@ -249,6 +315,9 @@ def main():
                     help="sensitivity runs only: pages in allocation order instead of the "
                          "shuffled pool SURVEY §8d measures on")
     args = ap.parse_args()
+    if args.cpu_baseline_child:  # cpu_baseline()'s child: no torch, no GPU
+        print(json.dumps(cpu_baseline_run(CONFIGS[args.config], args.cpu_budget)), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -303,15 +372,19 @@ def main():
         shard_rows=shard_rows, gather=args.gather if world > 1 else "none",
         staging="host" if host_gather else "device")
     tokens = np.random.default_rng(args.seed + rank).integers(0, cfg["V"], B).astype(np.int32)
+    step_times = None if host_gather else []
     elapsed = dist_decode.timed_run(sd, args.warmup, args.steps, list(map(int, tokens)),
-                                    timer_device="cpu" if host_gather else "cuda")
+                                    timer_device="cpu" if host_gather else "cuda",
+                                    step_times=step_times)
     t_step = elapsed / args.steps
     T_mean = T + args.warmup + args.steps / 2.0
     value = (args.global_batch if strong else B * world) / t_step
 
-    # roofline of the dominant kernel (paged attention), timed live
+    # roofline of the dominant kernel (paged attention): the step's own launch,
+    # timed live
     T_now = dec.context_len(0)
-    t_attn = time_attention(dec, cfg, B, T_now, max_seq, row_group=cfg.get("beams", 1))
+    nsplit, form = dec.attention_plan()
+    t_attn = time_attention(dec)
     attn_b = attention_launch_bytes(cfg, T_now, B, unique=True)
     achieved = attn_b / t_attn / 1e9
     ratio = load_traffic(args.config)
@@ -325,21 +398,23 @@ def main():
                                "(2*FETCH_SIZE + WRITE_SIZE) / algorithmic bytes, committed, "
                                "times this launch's algorithmic bytes (not measured in this run)")
             if ratio else None,
-            "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}> + pa_merge_kernel",
+            "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}>"
+                      + (" beam-group" if form & 16 else "") + ": " + FORM_NAMES[form & 15]
+                      + f", {nsplit} splits (the step's own launch, llm_decoder_run_attention)",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
     if "beams" in cfg:  # logical bytes: every beam reads its whole context
         logical = attention_launch_bytes(cfg, T_now, B)
         roof["bytes_note"] = "achieved counts shared prefix pages once per sequence"
         roof["logical_bytes_per_launch"] = logical
         roof["logical_GBps"] = round(logical / t_attn / 1e9, 1)
-        t_plain = time_attention(dec, cfg, B, T_now, max_seq, row_group=1)
-        roof["ungrouped_launch_us"] = round(t_plain * 1e6, 2)  # same launch, plain schedule
+        t_plain = time_attention_plain(dec, cfg, B, T_now, max_seq)
+        roof["ungrouped_launch_us"] = round(t_plain * 1e6, 2)  # plain schedule, fp32 out
     step_b = step_bytes(cfg, T_mean, B)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(cfg, args.cpu_budget)
+            cpu = cpu_baseline(args.config, args.cpu_budget)
         except Exception as ex:  # the baseline never blocks the GPU number
             log(f"cpu baseline failed: {ex!r}")
     if rank == 0:
@@ -352,6 +427,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
+            "ms_per_step_median_hip_events": round(float(np.median(step_times)) * 1e3, 4)
+            if step_times else None,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,

@@ -80,6 +80,20 @@ size_t pa_decode_workspace_bytes(int B, int H, int D, int max_tiles, int pages_p
  * context, so the two can differ.  For labelling runs, not for sizing them. */
 int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles);
 
+/* The launch a pa_decode / pa_decode_grouped call with these arguments
+ * takes, without launching it: *nsplit = splits per (row, head) and *form =
+ * LLM_PA_FORM_* (direct: one split, no merge; split + merge launch;
+ * LLM_PA_FORM_BEAM is or-ed in for the beam-group kernel).  For tests and
+ * run labels; the decoder's own step reports its launch with
+ * llm_decoder_attention_plan. */
+#define LLM_PA_FORM_DIRECT 0
+#define LLM_PA_FORM_SPLIT_MERGE 1     /* split launch + pa_merge_kernel (fp32 rows) */
+#define LLM_PA_FORM_SPLIT_MERGE_ROW 2 /* split launch + pa_merge_row_kernel (o_proj input) */
+#define LLM_PA_FORM_WG_MERGE 3        /* splits merged inside the split workgroup */
+#define LLM_PA_FORM_BEAM 16
+int pa_decode_plan(const pa_kv_view* kv, int B, int H, int D, int T, int pages_per_split,
+                   int row_group, int* nsplit, int* form);
+
 /* Paged decode attention (replaces paged_flash_attention_kernel_fused,
  * attention/paged_flash_attention_kernel_fused.cu:5-90, launched by
  * AttentionTileLauncher::launch, attention/attention_tile_launcher.hpp:36-89,
@@ -91,8 +105,11 @@ int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles)
  *                                           the reference's double division)
  *   out[b,h] = sum_t exp(s_t - max s) v_t / (sum_t exp(s_t - max s) + 1e-6)
  * over t < T_b whose page is present.  q, out: fp32 [B][H][D] device.
- * pages_per_split <= 0 selects pa_decode_pages_per_split().  workspace may be
- * NULL when the call needs none (single split). */
+ * pages_per_split <= 0: the split count is chosen on the device side of the
+ * call from the launch's occupancy (a whole number of resident-wave rounds)
+ * and each row's split length from its own context; pa_decode_pages_per_split
+ * only estimates it, and pa_decode_plan reports the choice exactly.
+ * workspace may be NULL when the call needs none (single split). */
 int pa_decode(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
               const int32_t* context_lens, int B, int H, int D, int T, float sm_scale,
               int pages_per_split, void* workspace, size_t workspace_bytes, void* stream);
@@ -414,7 +431,7 @@ int llm_decoder_sync(llm_decoder* d);
  * next ids (int32 [batch], the greedy argmax or the sampled ids) to dst_dev:
  * the ids-only gather of the multi-GPU path without a host sync. */
 int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* stream);
-/* Activation taps for parity checks (INT8 decoders): every following
+/* Activation taps for parity checks: every following
  * llm_decoder_step also copies, per layer l and stage s (0: LN1 output, 1:
  * attention output, 2: LN2 output, 3: fc1 output -- the four int8 GEMM inputs
  * of DecoderBlock::forward, decoder/decoder_block.hpp:43-61), the rows' int8
@@ -423,8 +440,20 @@ int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* stream);
  *                                                           inter_dim at s = 3;
  *   slot stride ceil(max_batch/16)*16 * max(hidden_dim, inter_dim) bytes)
  * and their fp32 dequantisation scales to s_dev[(l*4 + s) * max_batch + row].
+ * FP16 decoders (CUDADecoder) tap stage 1 only -- the merged attention rows as
+ * the fp16 o_proj input, packed-A order (a_frag_off_f16), at the same slot
+ * layout with 2 bytes per element; s_dev is not written.
  * Both NULL switches the taps off.  Prefill chunks are not tapped. */
 int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev);
+/* The attention launch of the decoder's step at its current batch and row
+ * group (pa_decode_plan of layer 0's view, T = max_seq_len: the step graph's
+ * launch, whose split lengths follow each row's live context). */
+int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form);
+/* Enqueue layer `layer`'s attention launch of the decoder's step on `stream`
+ * (NULL: the decoder's) -- the same kernels, grid and outputs as inside the
+ * step graph (q from the last step's projection, each row's live context, the
+ * o_proj input written), for timing the step's own launch in isolation. */
+int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream);
 int llm_decoder_context_len(const llm_decoder* d, int row);
 kv_cache* llm_decoder_kv(llm_decoder* d);
 

@@ -444,29 +444,42 @@ uint16_t* oracle_decoder_kv_ptr(void* h, int layer, int which) {
 // (one LSB); forcing keeps such a flip from propagating, so the rest of the
 // step is compared at full precision.  stats [L][4][3]: number of int8 values
 // that differ, their max |difference|, max rel. difference of the scales.
+// attn_out (optional, [L][B][hid] fp32): every layer's attention output before
+// the o_proj input conversion (int8 quantisation or the fp16 rounding of the
+// CUDADecoder), for checks of the GPU's merged attention rows.
 static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
                         int32_t* next_out, const int8_t* forced_q, const float* forced_s,
-                        float* stats);
+                        float* stats, float* attn_out);
 
 int oracle_decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
                         int32_t* next_out) {
   return decoder_step(handle, tokens, pos, attn_scale, layers_to_run, do_lm_head, x_out,
-                      logits_out, next_out, nullptr, nullptr, nullptr);
+                      logits_out, next_out, nullptr, nullptr, nullptr, nullptr);
 }
 
 int oracle_decoder_step_forced(void* handle, const int32_t* tokens, const int32_t* pos,
                                float attn_scale, float* logits_out, int32_t* next_out,
                                const int8_t* forced_q, const float* forced_s, float* stats) {
   return decoder_step(handle, tokens, pos, attn_scale, -1, 1, nullptr, logits_out, next_out,
-                      forced_q, forced_s, stats);
+                      forced_q, forced_s, stats, nullptr);
+}
+
+// oracle_decoder_step / _step_forced with the per-layer attention outputs
+// (forced_q NULL: a free step; the fp16 CUDADecoder restatement takes no forcing)
+int oracle_decoder_step_attn(void* handle, const int32_t* tokens, const int32_t* pos,
+                             float attn_scale, float* logits_out, int32_t* next_out,
+                             const int8_t* forced_q, const float* forced_s, float* stats,
+                             float* attn_out) {
+  return decoder_step(handle, tokens, pos, attn_scale, -1, 1, nullptr, logits_out, next_out,
+                      forced_q, forced_s, stats, attn_out);
 }
 
 static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
                         int32_t* next_out, const int8_t* forced_q, const float* forced_s,
-                        float* stats) {
+                        float* stats, float* attn_out) {
   auto* d = static_cast<OracleDecoder*>(handle);
   const oracle_model& m = d->m;
   const int B = d->B, H = m.H, D = m.D, hid = m.hid, inter = m.inter;
@@ -553,6 +566,7 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
         }
       }
     }
+    if (attn_out) std::memcpy(attn_out + (size_t)l * B * hid, o.data(), sizeof(float) * B * hid);
     if (f16w) {
       f16_gemm(o.data(), B, hid, m.hwo + (size_t)l * hid * hid, hid, nullptr, 0, x.data());
       oracle_layer_norm(x.data(), B, hid, m.ln2_g + lh, m.ln2_b + lh, 1e-5f, a.data());
@@ -591,5 +605,10 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
 }
 
 int oracle_num_threads() { return omp_get_max_threads(); }
+// The CPU baseline sets its thread count explicitly (OMP_NUM_THREADS is read
+// once, when the OpenMP runtime starts, possibly before this library loads).
+void oracle_set_num_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+}
 
 }  // extern "C"

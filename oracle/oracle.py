@@ -125,7 +125,11 @@ class Oracle:
         L.oracle_decoder_step_forced.restype = ctypes.c_int
         L.oracle_decoder_step_forced.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_float,
                                                  _f32p, _i32p, _i8p, _f32p, _f32p]
+        L.oracle_decoder_step_attn.restype = ctypes.c_int
+        L.oracle_decoder_step_attn.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_float,
+                                               _f32p, _i32p, _i8p, _f32p, _f32p, _f32p]
         L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_set_num_threads.argtypes = [ctypes.c_int]
 
     # -- attention ---------------------------------------------------------
     def paged_attention(self, q, k_pool, v_pool, page_table, *, T, beam_ids=None,
@@ -281,6 +285,31 @@ class OracleDecoder:
         assert rc == 0, rc
         return logits, nxt, stats
 
+    def step_attn(self, tokens, pos, forced_q=None, forced_s=None, attn_scale=1.0):
+        """A step (teacher-forced when forced_q / forced_s are given, INT8
+        weights only) that also returns every layer's attention output before
+        the o_proj input conversion: (logits, next, stats or None, attn
+        [L][B][hid] fp32)."""
+        c = self.cfg
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        pos = np.ascontiguousarray(pos, np.int32)
+        logits = np.empty((self.B, c["V"]), np.float32)
+        nxt = np.empty(self.B, np.int32)
+        attn = np.empty((c["L"], self.B, c["hid"]), np.float32)
+        stats = fq = fs = None
+        if forced_q is not None:
+            fq = np.ascontiguousarray(forced_q, np.int8)
+            fs = np.ascontiguousarray(forced_s, np.float32)
+            assert fq.shape == (c["L"], 4, self.B, max(c["hid"], c["inter"])), fq.shape
+            assert fs.shape == (c["L"], 4, self.B), fs.shape
+            stats = np.zeros((c["L"], 4, 3), np.float32)
+        rc = self.o.lib.oracle_decoder_step_attn(
+            self.h, _ptr(tokens, _i32p), _ptr(pos, _i32p), attn_scale, _ptr(logits, _f32p),
+            _ptr(nxt, _i32p), _ptr(fq, _i8p), _ptr(fs, _f32p), _ptr(stats, _f32p),
+            _ptr(attn, _f32p))
+        assert rc == 0, rc
+        return logits, nxt, stats, attn
+
     def step(self, tokens, pos, attn_scale=1.0, layers=-1, lm_head=True):
         c = self.cfg
         tokens = np.ascontiguousarray(tokens, np.int32)
@@ -309,6 +338,17 @@ def unpack_a_i8(packed: np.ndarray, rows: int, K: int) -> np.ndarray:
     k = np.arange(K)[None, :]
     off = ((((m >> 4) * KS + (k >> 6)) * 64 + (m & 15) + 16 * ((k & 63) >> 4)) * 16 + (k & 15))
     return np.asarray(packed).reshape(-1)[off]
+
+
+def unpack_a_f16(packed: np.ndarray, rows: int, K: int) -> np.ndarray:
+    """[rows][K] fp16 from the packed-A order of the FP16 decoder's GEMM inputs
+    (csrc/common.hpp a_frag_off_f16: one 1 KiB block per (16-row tile, 32-k
+    step); lane l = row l&15 + 16 * ((k&31) >> 3), 8 consecutive k per lane)."""
+    KS = K // 32
+    m = np.arange(rows)[:, None]
+    k = np.arange(K)[None, :]
+    off = ((((m >> 4) * KS + (k >> 5)) * 64 + (m & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7))
+    return np.asarray(packed).reshape(-1).view(np.float16)[off]
 
 
 def dnnl_matmul_int8_np(A, B, scaleA, scaleB, scaleC=1.0, bias=None, activation=""):

@@ -224,6 +224,16 @@ class Decoder {
     check(llm_decoder_set_taps(d_, reinterpret_cast<int8_t*>(q_ptr), reinterpret_cast<float*>(s_ptr)));
   }
   int context_len(int row) const { return llm_decoder_context_len(d_, row); }
+  void run_attention(int layer, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    check(llm_decoder_run_attention(d_, layer, reinterpret_cast<void*>(stream)));
+  }
+  // llm_decoder_attention_plan: (splits per (row, head), LLM_PA_FORM_*)
+  py::tuple attention_plan() {
+    int ns = 0, form = 0;
+    check(llm_decoder_attention_plan(d_, &ns, &form));
+    return py::make_tuple(ns, form);
+  }
   uintptr_t kv_handle() const { return reinterpret_cast<uintptr_t>(llm_decoder_kv(d_)); }
   const llm_decoder_config& config() const { return cfg_; }
 
@@ -425,6 +435,9 @@ PYBIND11_MODULE(llm_decoder, m) {
         .def("set_taps", &Decoder::set_taps, py::arg("q_ptr"), py::arg("s_ptr"))
         .def("copy_next_ids", &Decoder::copy_next_ids, py::arg("dst_ptr"), py::arg("stream") = 0)
         .def("context_len", &Decoder::context_len)
+        .def("attention_plan", &Decoder::attention_plan)
+        .def("run_attention", &Decoder::run_attention, py::arg("layer") = 0,
+             py::arg("stream") = 0)
         .def_property_readonly("kv_handle", &Decoder::kv_handle);
   };
   py::class_<Decoder>(m, "_Decoder");

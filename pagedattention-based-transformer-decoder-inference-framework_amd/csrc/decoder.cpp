@@ -128,7 +128,7 @@ struct llm_decoder {
   size_t b16 = 0;  // max_batch rounded up to 16-row tiles
 
   int layer_pre(int l, hipStream_t st, const struct Rows& R);
-  int layer_attn(int l, hipStream_t st, const struct Rows& R);
+  int layer_attn(int l, hipStream_t st, const struct Rows& R, PaPlan* plan = nullptr);
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -409,12 +409,12 @@ bool llm_decoder::split_k(const Rows& R, int N, int K) const {
          !ln_fusable(wdtype, R.n, hid) && gemm_kslices(N, R.n, K / 64) > 1;
 }
 
-int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
+int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
   view.page_table += (size_t)R.table_row0 * H * view.max_tiles;  // rows r0..
   view.num_beams -= R.table_row0;
-  if (R.prefill_row >= 0 && pa_prefill_supported(&view)) {
+  if (R.prefill_row >= 0 && pa_prefill_supported(&view) && !plan) {
     // one MFMA pass over the chunk (K/V pages read once per 32 queries), then
     // the o_proj input conversion the decode merge would have fused
     PaRowOutputs ro;
@@ -442,7 +442,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R) {
   }
   return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
-                            R.row_group, 0);
+                            R.row_group, plan);
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
@@ -454,7 +454,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.A = R.act;
   g.M = R.n;
   // o_proj: input produced (packed) by the attention merge
-  if (i8) RET_IF(tap(l, 1, R, hid, st));
+  RET_IF(tap(l, 1, R, hid, st));
   g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = R.x;
   if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
   if (split_k(R, hid, hid)) {  // partials -> LN2 (x rebuilt there)
@@ -519,15 +519,21 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
 // Tap stage `stage` of layer l (0: LN1 out, 1: attention out, 2: LN2 out,
 // 3: fc1 out): the rows' packed int8 activations (K per row) and row scales.
 // Decode rows only (prefill chunks are not tapped); captured into the graph.
+// FP16 decoders: stage 1 only (the merged attention rows as the packed fp16
+// o_proj input, 2 bytes per element, no scales).
 int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
   if (!tap_q || R.prefill_row >= 0 || R.beam_rows) return LLM_OK;
+  const bool f16 = wdtype == LLM_F16;
+  if (f16 && stage != 1) return LLM_OK;
+  const size_t es = f16 ? 2 : 1;
   const size_t slot = (size_t)l * 4 + stage;
   const size_t n16 = ((size_t)R.n + 15) / 16 * 16;
   const size_t r0 = (size_t)R.table_row0;  // rows r0.. of the step (16-row aligned)
-  LLM_HIP_RET(hipMemcpyAsync(tap_q + slot * b16 * qa_ld + r0 * K, R.act, n16 * K,
+  LLM_HIP_RET(hipMemcpyAsync(tap_q + (slot * b16 * qa_ld + r0 * K) * es, R.act, n16 * K * es,
                              hipMemcpyDeviceToDevice, st));
-  LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, R.sa, sizeof(float) * R.n,
-                             hipMemcpyDeviceToDevice, st));
+  if (!f16)
+    LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, R.sa, sizeof(float) * R.n,
+                               hipMemcpyDeviceToDevice, st));
   return LLM_OK;
 }
 
@@ -823,13 +829,33 @@ extern "C" int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev)
   LLM_REQUIRE(d, "llm_decoder_set_taps: NULL");
   LLM_REQUIRE((q_dev == nullptr) == (s_dev == nullptr),
               "llm_decoder_set_taps: give both tap buffers or neither");
-  LLM_REQUIRE(!q_dev || d->wdtype == LLM_I8, "llm_decoder_set_taps: INT8 decoders only");
   std::lock_guard<std::mutex> g(d->mu);
   LLM_HIP_RET(hipStreamSynchronize(d->stream));
   d->tap_q = q_dev;
   d->tap_s = s_dev;
   d->graph_batch = -1;  // the step graph gains / loses the tap copies
   return LLM_OK;
+}
+
+extern "C" int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form) {
+  LLM_REQUIRE(d && nsplit && form, "llm_decoder_attention_plan: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_REQUIRE(d->batch > 0, "llm_decoder_attention_plan: no active rows");
+  const Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
+  PaPlan p;
+  RET_IF(d->layer_attn(0, d->stream, R, &p));
+  *nsplit = p.nsplit;
+  *form = p.form;
+  return LLM_OK;
+}
+
+extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream) {
+  LLM_REQUIRE(d, "llm_decoder_run_attention: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_REQUIRE(d->batch > 0, "llm_decoder_run_attention: no active rows");
+  LLM_REQUIRE(layer >= 0 && layer < d->L, "llm_decoder_run_attention: layer out of range");
+  hipStream_t st = stream ? as_stream(stream) : d->stream;
+  return d->layer_attn(layer, st, d->step_rows(0, d->batch, d->attn_ws.p));
 }
 
 extern "C" int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,

@@ -20,6 +20,7 @@
 #include <fstream>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "common.hpp"
@@ -368,6 +369,17 @@ extern "C" int kv_cache_load_pools(kv_cache* c, const char* path) {
   const size_t pb = k.page_bytes();
   const long long want = 2LL * k.num_pages * (long long)pb;
   const long long size = file_size(f);
+  uint64_t magic = 0;
+  if (size >= 8) {
+    f.read(reinterpret_cast<char*>(&magic), sizeof(magic));
+    f.seekg(0, std::ios::beg);
+  }
+  // a page-table snapshot (kv_cache_save; round-1 bindings' default format)
+  if (size != want && (magic == kMagic || magic == kMagicV2))
+    return fail(LLM_ERR_IO, std::string("kv_cache_load_pools: ") + path +
+                                " is a page-table snapshot (APPIMKV), not a pool dump: load it "
+                                "with kv_cache_load (KVTileCache.load_from_file(path, "
+                                "format='snapshot'))");
   // the reference reads whatever is there (kv_tile_cache.cpp:121-122); a dump
   // of another pool size is refused here before any page changes
   if (size != want)
@@ -465,6 +477,32 @@ extern "C" int kv_cache_load_tiles(kv_cache* c, int layer, int kind, const char*
       seen.push_back({k.index(layer, idx[3 * i], idx[3 * i + 1], idx[3 * i + 2]), i});
     std::stable_sort(seen.begin(), seen.end(),
                      [](const auto& a, const auto& b) { return a.first < b.first; });
+    // the pages the load needs (unmapped tiles, and copy-on-write copies of
+    // shared ones, counting each shared page's references down as its tiles
+    // are un-shared) must all be free BEFORE anything is allocated: a load that
+    // fails leaves the cache unchanged
+    long long need = 0;
+    {
+      std::unordered_map<int32_t, int32_t> refs;
+      for (size_t j = 0; j < seen.size(); ++j) {
+        if (j + 1 < seen.size() && seen[j + 1].first == seen[j].first) continue;
+        const int32_t p = k.h_table[seen[j].first];
+        if (p < 0) {  // ensure_tile allocates
+          ++need;
+          continue;
+        }
+        auto it = refs.find(p);
+        if (it == refs.end()) it = refs.emplace(p, k.refcount[p]).first;
+        if (it->second > 1) {
+          ++need;
+          --it->second;
+        }
+      }
+    }
+    if (need > k.free_count())
+      return fail(LLM_ERR_OOM, "kv_cache_load_tiles: the load needs " + std::to_string(need) +
+                                   " free pages, the pool has " + std::to_string(k.free_count()) +
+                                   " (cache unchanged)");
     for (size_t j = 0; j < seen.size(); ++j) {
       if (j + 1 < seen.size() && seen[j + 1].first == seen[j].first) continue;  // superseded
       const int i = seen[j].second;

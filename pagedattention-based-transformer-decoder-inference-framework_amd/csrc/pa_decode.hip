@@ -1242,8 +1242,7 @@ long long resident_waves() {
 // split balance 64/16.
 bool beam_mfma_on() {
 #if LLM_TUNING
-  static const bool v = env_int("LLM_BEAM_MFMA", 0) != 0;
-  return v;
+  return env_int("LLM_BEAM_MFMA", 0) != 0;  // read per launch: a test sets and restores it
 #else
   return false;
 #endif
@@ -1266,17 +1265,12 @@ int beam_mfma_balance16() {
 #endif
 }
 
-// lean = the low-register form (one 8 KiB register stage, 8 waves per SIMD
-// requested): same stream rate measured (scripts/tune_attention.py variant 6
-// vs 1), used when the launch must leave CU room for kernels running beside
-// it (micro-batch overlap).
 template <int D, int TS, int KVT>
-hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_t st,
-                        bool* beam) {
+hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool* beam) {
   const int waves = ((a.B + a.group - 1) / a.group) * a.group * a.H * a.nsplit;
   const dim3 grid((waves + 3) / 4), block(256);
   if constexpr (KVT != LLM_F16) {
-    // other KV element types: the standard schedule (no lean / beam-prefetch forms)
+    // other KV element types: the standard schedule (no beam-prefetch form)
     constexpr int ST = split_stages<D, TS, KVT>();
     if (direct)
       hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 16384, kKvLoadAux, ST, 0, false, false, KVT>),
@@ -1287,13 +1281,13 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
     return hipGetLastError();
   }
   constexpr int ST = split_stages<D, TS, LLM_F16>();
-  if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct, not lean
+  if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
                                         LLM_F16, true, true>),
                        dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
     return hipGetLastError();
   }
-  if (a.group == 4 && !direct && !lean && ST == 2) {
+  if (a.group == 4 && !direct && ST == 2) {
     // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
     // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
     // 20 % parked (SQ PMC, scripts/gpu_sq_pmc.sh); same-box A/B of the C4
@@ -1322,14 +1316,6 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
                                         false, true>), grid, block, 0, st, a);
     *beam = true;
-  } else if (lean && TS * D * 2 <= 4096) {
-    // the 8-waves-per-SIMD register budget holds one stage of pages <= 4 KiB
-    if constexpr (TS * D * 2 <= 4096) {
-      if (direct)
-        hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
-      else
-        hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 8192, kKvLoadAux, 1, 8>), grid, block, 0, st, a);
-    }
   } else if (direct) {
     hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 16384, kKvLoadAux, ST>), grid, block, 0, st, a);
   } else {
@@ -1339,25 +1325,24 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, bool lean, hipStream_
 }
 
 template <int D, int KVT>
-hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, bool lean, hipStream_t st,
-                       bool* beam) {
+hipError_t dispatch_ts(const PaSplitArgs& a, int TS, bool direct, hipStream_t st, bool* beam) {
   constexpr int ES = kv_elem_bytes<KVT>();
   if (TS == 16) {
-    if constexpr (kv_shape_ok(D, 16, ES)) return launch_split<D, 16, KVT>(a, direct, lean, st, beam);
+    if constexpr (kv_shape_ok(D, 16, ES)) return launch_split<D, 16, KVT>(a, direct, st, beam);
   } else if (TS == 32) {
-    if constexpr (kv_shape_ok(D, 32, ES)) return launch_split<D, 32, KVT>(a, direct, lean, st, beam);
+    if constexpr (kv_shape_ok(D, 32, ES)) return launch_split<D, 32, KVT>(a, direct, st, beam);
   }
   return hipErrorInvalidValue;
 }
 
 template <int D>
-hipError_t dispatch_kvt(const PaSplitArgs& a, int kvt, int TS, bool direct, bool lean,
-                        hipStream_t st, bool* beam) {
+hipError_t dispatch_kvt(const PaSplitArgs& a, int kvt, int TS, bool direct, hipStream_t st,
+                        bool* beam) {
   switch (kvt) {
-    case LLM_F16: return dispatch_ts<D, LLM_F16>(a, TS, direct, lean, st, beam);
-    case LLM_BF16: return dispatch_ts<D, LLM_BF16>(a, TS, direct, lean, st, beam);
-    case LLM_F32: return dispatch_ts<D, LLM_F32>(a, TS, direct, lean, st, beam);
-    case LLM_I8: return dispatch_ts<D, LLM_I8>(a, TS, direct, lean, st, beam);
+    case LLM_F16: return dispatch_ts<D, LLM_F16>(a, TS, direct, st, beam);
+    case LLM_BF16: return dispatch_ts<D, LLM_BF16>(a, TS, direct, st, beam);
+    case LLM_F32: return dispatch_ts<D, LLM_F32>(a, TS, direct, st, beam);
+    case LLM_I8: return dispatch_ts<D, LLM_I8>(a, TS, direct, st, beam);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1586,12 +1571,13 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
                             int D, int T, float sm_scale, int pages_per_split, void* workspace,
                             size_t workspace_bytes, hipStream_t st, const PaRowOutputs* rows,
-                            int row_group, int waves_per_simd) {
+                            int row_group, PaPlan* plan) {
   LLM_REQUIRE(kv != nullptr, "pa_decode: kv view is NULL");
   LLM_REQUIRE(B >= 0 && H > 0 && D > 0 && T >= 0, "pa_decode: bad B/H/D/T");
+  if (plan) *plan = PaPlan{};
   if (B == 0) return LLM_OK;
   const bool row_out = rows && (rows->q || rows->out16);
-  LLM_REQUIRE(q != nullptr && (out != nullptr || row_out), "pa_decode: q/out NULL");
+  LLM_REQUIRE(plan || (q != nullptr && (out != nullptr || row_out)), "pa_decode: q/out NULL");
   LLM_REQUIRE(!rows || !rows->q || rows->inv_scale, "pa_decode: row quantisation needs inv_scale");
   LLM_REQUIRE(!row_out || (size_t)H * D * 4 <= 65536, "pa_decode: row outputs need H*D <= 16384");
   LLM_REQUIRE(!rows || !rows->pack || (H * D) % 64 == 0, "pa_decode: packed row outputs need H*D % 64 == 0");
@@ -1616,40 +1602,26 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // tiles at or past max_tiles have no page-table entry: they are missing (masked)
   const int ntiles_max = std::max(1, std::min((T + TS - 1) / TS, kv->max_tiles));
   const int pps_fixed = pages_per_split > 0 ? std::min(pages_per_split, kMaxPps) : 0;
-  // waves_per_simd > 0: lean kernel, splits sized for that many waves per SIMD
-  const bool lean = waves_per_simd > 0;
-  long long resident = 0;
-  if (pps_fixed <= 0) {
-    if (lean) {
-      int dev = 0, cus = 256;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-        (void)hipGetLastError();
-        cus = 256;
-      }
-      resident = (long long)cus * 4 * std::min(waves_per_simd, 8);
-    } else {
-      resident = resident_waves_for(D, TS, kv->kv_dtype);
-    }
-  }
+  const long long resident = pps_fixed <= 0 ? resident_waves_for(D, TS, kv->kv_dtype) : 0;
   // beam-group launches size their splits for the beam kernel's occupancy
   // (4 waves per SIMD against the plain kernel's 2: C4 8 splits, not 4)
-  if (pps_fixed <= 0 && !lean && row_group == 4 && kv->kv_dtype == LLM_F16)
-    resident = std::max(resident, beam_resident_waves_for(D, TS));
+  const long long resident_launch =
+      pps_fixed <= 0 && row_group == 4 && kv->kv_dtype == LLM_F16
+          ? std::max(resident, beam_resident_waves_for(D, TS)) : resident;
   // fp16 o_proj input only (the FP16 decoder's attention): with at most one
   // merge batch of splits per (b, h) the splits merge inside the split
   // launch's workgroup (C2: 12 merge launches per step fewer), with long splits
-  const bool wgm_ok = row_out && rows->out16 && !rows->q && row_group == 1 && !lean &&
+  const bool wgm_ok = row_out && rows->out16 && !rows->q && row_group == 1 &&
                       kv->kv_dtype == LLM_F16 && wg_merge_on();
-  int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident);
+  int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident_launch);
   if (wgm_ok && pps_fixed <= 0) {
-    const int nw = choose_nsplit(B, H, ntiles_max, 0, resident, kWgmShortPps);
+    const int nw = choose_nsplit(B, H, ntiles_max, 0, resident_launch, kWgmShortPps);
     if (nw >= 2 && nw <= kWgmMaxSplits) nsplit = nw;
   }
 #if LLM_TUNING
   // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
   // eligible launches (fp16 row outputs, dynamic splits)
-  if (rows && rows->out16 && !rows->q && row_group == 1 && pps_fixed <= 0 && !lean) {
+  if (rows && rows->out16 && !rows->q && row_group == 1 && pps_fixed <= 0) {
     const int f = env_int("LLM_WGM_SPLITS", 0);
     if (f >= 2 && f <= kWgmMaxSplits && (long long)f * kMaxPps >= ntiles_max) nsplit = f;
   }
@@ -1659,6 +1631,17 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                 "pa_decode: at most 128 splits of at most 128 pages per row (raise "
                 "pages_per_split, or pass 0; T <= 16384 pages)");
   const bool direct = nsplit <= 1;
+  if (plan) {
+    const int group = std::max(1, std::min(row_group, 4));
+    const bool wg = wgm_ok && !direct && group == 1 && nsplit <= kWgmMaxSplits;
+    const bool beam = group == 4 && !direct && kv->kv_dtype == LLM_F16 &&
+                      TS * D * 2 <= 8192;
+    plan->nsplit = nsplit;
+    plan->form = (direct ? LLM_PA_FORM_DIRECT : wg ? LLM_PA_FORM_WG_MERGE
+                  : row_out ? LLM_PA_FORM_SPLIT_MERGE_ROW : LLM_PA_FORM_SPLIT_MERGE) |
+                 (beam ? LLM_PA_FORM_BEAM : 0);
+    return LLM_OK;
+  }
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
 
   PaSplitArgs a{};
@@ -1699,10 +1682,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   hipError_t e;
   bool beam = false;  // the beam kernel ran: every split holds a partial
   switch (D) {
-    case 32: e = dispatch_kvt<32>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
-    case 64: e = dispatch_kvt<64>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
-    case 128: e = dispatch_kvt<128>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
-    default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, lean, st, &beam); break;
+    case 32: e = dispatch_kvt<32>(a, kv->kv_dtype, TS, direct, st, &beam); break;
+    case 64: e = dispatch_kvt<64>(a, kv->kv_dtype, TS, direct, st, &beam); break;
+    case 128: e = dispatch_kvt<128>(a, kv->kv_dtype, TS, direct, st, &beam); break;
+    default: e = dispatch_kvt<256>(a, kv->kv_dtype, TS, direct, st, &beam); break;
   }
   if (e != hipSuccess) return fail(LLM_ERR_HIP, std::string("pa_split launch: ") + hipGetErrorString(e));
   if (wgm) return LLM_OK;
@@ -1733,6 +1716,18 @@ extern "C" int pa_decode_grouped(const pa_kv_view* kv, const float* q, float* ou
   return pa_decode_internal(kv, q, H * D, out, beam_ids, context_lens, B, H, D, T, sm_scale,
                             pages_per_split, workspace, workspace_bytes, as_stream(stream),
                             nullptr, row_group);
+}
+
+extern "C" int pa_decode_plan(const pa_kv_view* kv, int B, int H, int D, int T,
+                              int pages_per_split, int row_group, int* nsplit, int* form) {
+  LLM_REQUIRE(nsplit && form, "pa_decode_plan: NULL output");
+  LLM_REQUIRE(row_group >= 1 && row_group <= 4, "pa_decode_plan: row_group must be in [1, 4]");
+  PaPlan p;
+  const int rc = pa_decode_internal(kv, nullptr, H * D, nullptr, nullptr, nullptr, B, H, D, T, 1.f,
+                                    pages_per_split, nullptr, 0, nullptr, nullptr, row_group, &p);
+  *nsplit = p.nsplit;
+  *form = p.form;
+  return rc;
 }
 
 extern "C" int pa_decode(const pa_kv_view* kv, const float* q, float* out,

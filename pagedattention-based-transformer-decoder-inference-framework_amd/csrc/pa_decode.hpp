@@ -19,13 +19,21 @@ struct PaRowOutputs {
   int keep_out = 1;  // 0: a split launch skips the fp32 `out` rows (only q / out16 are read)
 };
 
+// The launch a call takes (pa_decode_plan): splits per (row, head) and
+// LLM_PA_FORM_* (| LLM_PA_FORM_BEAM).
+struct PaPlan {
+  int nsplit = 0;
+  int form = 0;
+};
+
 // `out` (fp32) may be NULL when `rows` requests an output and the launch splits.
+// plan != NULL: only report the launch (q / out / workspace are not needed).
 int pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float* out,
                        const int32_t* beam_ids, const int32_t* context_lens, int B, int H, int D,
                        int T, float sm_scale, int pages_per_split, void* workspace,
                        size_t workspace_bytes, hipStream_t st,
                        const PaRowOutputs* rows = nullptr, int row_group = 1,
-                       int waves_per_simd = 0);
+                       PaPlan* plan = nullptr);
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 
 // Split merge of per-(row, head, split) partial softmax states into rows

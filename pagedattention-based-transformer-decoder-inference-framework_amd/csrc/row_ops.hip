@@ -173,11 +173,14 @@ __global__ __launch_bounds__(kRowThreads) void quantize_rows_v_kernel(
 // LayerNorm<T>::forward (decoder/layer_norm.hpp:20-37) and int8_quant.cpp as
 // ln_wave.hpp (the GEMM prologue); only the fp32 summation order differs.
 // q / out16 in packed-A order when pack.
+// inv_scale is NOT __restrict__: with split-K partials pp.sa (the GEMM's row
+// scales) is the same buffer the row's new scale is written to; every read of
+// pp.sa comes before the block reductions that the write depends on.
 template <int VPT>
 __global__ __launch_bounds__(kRowThreads) void layernorm_rows_kernel(
     const float* __restrict__ x, int rows, int cols, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
-    float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack, LnPartials pp) {
+    float* inv_scale, _Float16* __restrict__ out16, int pack, LnPartials pp) {
   __shared__ float sh[4];
   const int r = blockIdx.x;
   const int n4 = cols >> 2;

@@ -178,11 +178,15 @@ class ShardedDecode:
 
 
 def timed_run(sd: ShardedDecode, warmup: int, steps: int, first_tokens, *,
-              sync: Callable[[], None] | None = None, timer_device="cuda") -> float:
+              sync: Callable[[], None] | None = None, timer_device="cuda",
+              step_times: list | None = None) -> float:
     """bench.py's measured loop: `warmup` untimed steps (the first feeds
     first_tokens, later steps feed back the device's ids), then exactly `steps`
     timed ones bracketed by a barrier + device synchronisation on both sides.
-    Returns the elapsed seconds, the MAX over ranks."""
+    Returns the elapsed seconds, the MAX over ranks.  step_times (a list, GPU
+    ranks only): filled with this rank's per-step device times in seconds,
+    from HIP events recorded on torch's current stream (the stream the steps
+    run on) between consecutive steps."""
     import torch
     import torch.distributed as dist
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -195,15 +199,24 @@ def timed_run(sd: ShardedDecode, warmup: int, steps: int, first_tokens, *,
     if multi:
         dist.barrier()
     sync()
+    ev = None
+    if step_times is not None:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
+    if ev:
+        ev[0].record()
     for i in range(steps):
         sd.step(first_tokens if warmup == 0 and i == 0 else None)
+        if ev:
+            ev[i + 1].record()
     sd.finish()
     sync()
     if multi:
         dist.barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    if ev:
+        step_times[:] = [ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(steps)]
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device=timer_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -55,6 +55,8 @@ _SIGS = {
     "llm_abi_version": (c_int, []),
     "pa_decode_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pa_decode_pages_per_split": (c_int, [c_int, c_int, c_int, c_int, c_int]),
+    "pa_decode_plan": (c_int, [ctypes.POINTER(PaKvView), c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_i32p, c_i32p]),
     "pa_decode": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_float, c_int, c_void_p, c_size_t,
                           c_void_p]),

@@ -47,6 +47,76 @@ def tiles_to_pool(k_tiles, v_tiles, present, *, seed=7, extra_pages=3):
 
 
 def rel_err(a, b):
+    """Tensor-normalised error max|a - b| / max|b|."""
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def elem_err(a, b, rtol=1e-3, atol_frac=1e-6, axis=None):
+    """Worst elementwise ratio |a - b| / (rtol |b| + atol_frac max|b|) (<= 1
+    passes): every element within rtol of its own value, with an absolute
+    floor of atol_frac of the largest |b| (of the whole tensor, or of each
+    slice along `axis`, e.g. per logit row)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = np.max(np.abs(b), axis=axis, keepdims=axis is not None) if b.size else 0.0
+    tol = rtol * np.abs(b) + atol_frac * np.maximum(scale, 1e-30)
+    return float(np.max(np.abs(a - b) / tol)) if b.size else 0.0
+
+
+def assert_parity(a, b, rtol=1e-3, atol_frac=1e-6, axis=None, what=""):
+    """The north_star's "1e-3 rel" as both bounds: tensor-normalised
+    (rel_err < rtol) and elementwise (|a - b| <= rtol |b| + atol_frac max|b|,
+    SURVEY Appendix B.1)."""
+    r = rel_err(a, b)
+    e = elem_err(a, b, rtol, atol_frac, axis)
+    assert r < rtol, f"{what} rel_err {r:.3e} >= {rtol}"
+    if e > 1.0:
+        a64, b64 = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        i = np.unravel_index(np.argmax(np.abs(a64 - b64) / (rtol * np.abs(b64) + 1e-300)), b64.shape)
+        raise AssertionError(f"{what} elementwise bound exceeded x{e:.2f} "
+                             f"(worst rel element {i}: {a64[i]!r} vs {b64[i]!r}; rel_err {r:.3e})")
+
+
+def hip_copy_to_host(dst: np.ndarray, src_ptr: int) -> None:
+    """hipMemcpy device -> host of dst.nbytes bytes (tests that read the
+    decoder's pools and page tables back)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipMemcpy.restype = ctypes.c_int
+    assert hip.hipMemcpy(dst.ctypes.data, ctypes.c_void_p(src_ptr), dst.nbytes, 2) == 0
+
+
+def decoder_kv_to_oracle(dec, odec, rows, T):
+    """Copy the decoder's paged KV context (positions [0, T) of every row, every
+    layer, read back from its page pools through its page table) into the
+    oracle decoder's contiguous KV (OracleDecoder.kv).  Returns the number of
+    distinct pages read per layer (beam forks share pages)."""
+    import ctypes
+    import llm_capi
+    lib = llm_capi.load()
+    kvh = ctypes.c_void_p(dec.kv_handle)
+    view = llm_capi.PaKvView()
+    llm_capi.check(lib.kv_cache_view(kvh, 0, ctypes.byref(view)))
+    ts, D, H, mt = view.page_size, view.head_dim, view.num_heads, view.max_tiles
+    n_pages = lib.kv_cache_num_pages(kvh)
+    stride = lib.kv_cache_page_stride(kvh)  # bytes from page to page (K page | V page)
+    assert stride == 2 * ts * D * 2, stride
+    pool = np.empty((n_pages, 2, ts, D), np.float16)
+    hip_copy_to_host(pool, lib.kv_cache_k_pool(kvh))
+    nt = (T + ts - 1) // ts
+    c = odec.cfg
+    distinct = []
+    for layer in range(c["L"]):
+        pt = np.empty((view.num_beams, H, mt), np.int32)
+        hip_copy_to_host(pt, lib.kv_cache_page_table(kvh, layer))
+        ids = pt[:rows, :, :nt]
+        assert (ids >= 0).all() and (ids < n_pages).all()
+        distinct.append(len(np.unique(ids)))
+        for which in (0, 1):
+            kv = odec.kv(layer, which)  # [B][H][max_seq][D]
+            pages = pool[ids, which]    # [rows][H][nt][ts][D]
+            kv[:rows, :, :T] = pages.reshape(rows, H, nt * ts, D)[:, :, :T]
+    return distinct

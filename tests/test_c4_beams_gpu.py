@@ -13,7 +13,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from _util import rel_err
+from _util import assert_parity, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -79,8 +79,8 @@ def test_c4_beam_group_attention_vs_oracle(gpu, oracle, layer):
                                 layer, row, head, nt, D, ts)
         sub_pt = np.arange(nt, dtype=np.int32).reshape(1, 1, nt)
         ref = oracle.paged_attention(qh[row:row + 1, head:head + 1], kk, vv, sub_pt, T=T)
-        assert rel_err(outs[W][row, head], ref[0, 0]) < 1e-3, (row, head)
-        assert rel_err(outs[1][row, head], ref[0, 0]) < 1e-3, (row, head)
+        assert_parity(outs[W][row, head], ref[0, 0], 1e-3)
+        assert_parity(outs[1][row, head], ref[0, 0], 1e-3)
 
 
 @pytest.mark.parametrize("B,T,shared,equal", [
@@ -89,7 +89,7 @@ def test_c4_beam_group_attention_vs_oracle(gpu, oracle, layer):
     (12, 330, 20, False),  # ragged contexts: one wave per beam, own pages
     (8, 4096, 240, True),  # C4 shape per sequence, 2 sequences
 ])
-def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal):
+def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     """The beam-group attention launch (row_group 4, fp16, D 128, page 16) on
     the cases its schedule branches on: partial groups, sub-page contexts and
     empty splits, ragged contexts, beam_ids routing inside a group, a missing
@@ -148,16 +148,15 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal):
     outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
                               beam_ids=d(beam_ids), row_group=4).cpu().numpy()
     assert np.isfinite(outg).all()
-    assert rel_err(plain, ref) < 1e-3
-    assert rel_err(outg, ref) < 1e-3
+    assert_parity(plain, ref, 1e-3)
+    assert_parity(outg, ref, 1e-3)
     assert rel_err(outg, plain) < 1e-5
     # the tuning build's MFMA beam kernel (not in the product library; its
-    # switch is read once per process, before the tuning build's first launch)
-    import os
-    os.environ["LLM_BEAM_MFMA"] = "1"
+    # switch is read per launch, and restored when the test ends)
+    monkeypatch.setenv("LLM_BEAM_MFMA", "1")
     outm = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
                               beam_ids=d(beam_ids), row_group=4,
                               lib=llm_capi.load_tune()).cpu().numpy()
     assert np.isfinite(outm).all()
-    assert rel_err(outm, ref) < 1e-3
+    assert_parity(outm, ref, 1e-3)
     assert rel_err(outm, plain) < 1e-5

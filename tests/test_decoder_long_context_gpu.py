@@ -1,0 +1,219 @@
+"""The decoder's OWN attention epilogue against the oracle at the split counts
+the BASELINE configs run.
+
+Inside a decode step the paged attention runs split-T: many splits per (row,
+head), merged by pa_merge_row_kernel, which also quantises each row (all
+heads) into the packed int8 o_proj input (INT8Decoder), or merged inside the
+split workgroup into the packed fp16 o_proj input (CUDADecoder, workgroup
+merge).  That merge is the reference's AV-and-store
+(attention_cpu/cpu_attention_kernel.cpp:103-120) followed by the quantiser
+(attention_cpu/int8_quant.cpp:5-13,59-64).
+
+Each test starts the decoder at a long context (llm_decoder_begin_synthetic /
+begin_beams: seeded random K/V in shuffled pages), reads every row's pages
+back through the page table into the oracle's contiguous KV
+(_util.decoder_kv_to_oracle), and steps GPU and oracle together:
+  * INT8: teacher forced at the four int8 GEMM inputs (taps); stage 1 (the
+    o_proj input = the merged, quantised attention rows) within one LSB of the
+    oracle's own quantisation of its fp32 attention, < 1e-3 of the values
+    flipped; logits at the north_star bar (1e-3, tensor and elementwise per
+    row), tokens exact unless tied.
+  * FP16: the tapped packed fp16 attention rows against the oracle's fp32
+    attention at 1e-3 (tensor and elementwise), and against its fp16 rounding
+    (at most one fp16 ulp where the fp32 sums round differently); logits 1e-3.
+The split count of the step's own launch is read from the decoder
+(llm_decoder_attention_plan) and asserted, so the multi-split merge is what
+is compared."""
+import numpy as np
+import pytest
+
+from _util import assert_parity, decoder_kv_to_oracle, rel_err
+
+pytestmark = pytest.mark.gpu
+LOGIT_TOL = 1e-3
+TIE_TOL = 1e-5
+FORM_DIRECT, FORM_SPLIT_MERGE, FORM_SPLIT_MERGE_ROW, FORM_WG_MERGE, FORM_BEAM = 0, 1, 2, 3, 16
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class _Taps:
+    """llm_decoder_set_taps buffers (INT8: int8 + scales; FP16: stage 1 as fp16)."""
+
+    def __init__(self, dec, c, max_batch, f16=False):
+        torch = _torch()
+        self.L, self.hid, self.inter, self.f16 = c["L"], c["hid"], c["inter"], f16
+        self.K = max(self.hid, self.inter)
+        self.b16 = (max_batch + 15) // 16 * 16
+        self.maxB = max_batch
+        es = 2 if f16 else 1
+        self.q = torch.zeros(self.L * 4 * self.b16 * self.K * es, dtype=torch.int8, device="cuda")
+        self.s = torch.zeros(self.L * 4 * max_batch, dtype=torch.float32, device="cuda")
+        dec.set_taps(self.q.data_ptr(), self.s.data_ptr())
+
+    def read_i8(self, B):
+        from oracle.oracle import unpack_a_i8
+        q = self.q.cpu().numpy().reshape(self.L, 4, self.b16 * self.K)
+        s = self.s.cpu().numpy().reshape(self.L, 4, self.maxB)
+        fq = np.zeros((self.L, 4, B, self.K), np.int8)
+        for l in range(self.L):
+            for st in range(4):
+                Kst = self.inter if st == 3 else self.hid
+                fq[l, st, :, :Kst] = unpack_a_i8(q[l, st, :self.b16 * Kst], B, Kst)
+        return fq, np.ascontiguousarray(s[:, :, :B])
+
+    def read_attn_f16(self, B):
+        """Stage 1 of every layer: [L][B][hid] fp16 (the packed o_proj input)."""
+        from oracle.oracle import unpack_a_f16
+        q = self.q.cpu().numpy().view(np.uint16).reshape(self.L, 4, self.b16 * self.K)
+        return np.stack([unpack_a_f16(q[l, 1, :self.b16 * self.hid], B, self.hid)
+                         for l in range(self.L)])
+
+
+def _check_tokens(g_next, o_next, o_logits):
+    for b in range(len(g_next)):
+        if g_next[b] != o_next[b]:
+            gap = o_logits[b][o_next[b]] - o_logits[b][g_next[b]]
+            assert gap <= TIE_TOL * np.abs(o_logits[b]).max(), (b, gap)
+
+
+def _forced_steps_int8(dec, odec, taps, rows, T, steps, V, seed):
+    """GPU and teacher-forced oracle in lockstep from context T; returns the
+    stage-1 (attention) flip count, values compared, and the worst logit rel err."""
+    torch = _torch()
+    hid = odec.cfg["hid"]
+    logits = torch.empty((rows, V), device="cuda")
+    rng = np.random.default_rng(seed)
+    tok = [int(t) for t in rng.integers(0, V, rows)]
+    flips, vals, worst = 0, 0, 0.0
+    for s in range(steps):
+        g_next = dec.step(tok, logits_ptr=logits.data_ptr())
+        torch.cuda.synchronize()
+        fq, fs = taps.read_i8(rows)
+        o_logits, o_next, stats, attn = odec.step_attn(np.array(tok, np.int32),
+                                                       np.full(rows, T + s, np.int32), fq, fs)
+        # every int8 GEMM input within one LSB, row scales equal
+        assert stats[:, :, 1].max() <= 1, (s, stats)
+        assert stats[:, :, 2].max() < 1e-5, (s, stats)
+        assert np.isfinite(attn).all()
+        flips += int(stats[:, 1, 0].sum())
+        vals += odec.cfg["L"] * rows * hid
+        gl = logits.cpu().numpy()
+        assert_parity(gl, o_logits, LOGIT_TOL, axis=1, what=f"step {s} logits")
+        worst = max(worst, rel_err(gl, o_logits))
+        _check_tokens(g_next, o_next, o_logits)
+        tok = list(g_next)
+    return flips, vals, worst
+
+
+def _int8_decoder(oracle, L, H, D, V, max_seq, rows, seed):
+    import llm_decoder
+    from oracle.oracle import synthetic_int8_model
+    w = synthetic_int8_model(oracle, L=L, H=H, D=D, V=V, max_seq=max_seq, seed=seed)
+    c = w["cfg"]
+    dec = llm_decoder.INT8Decoder(c["L"], c["H"], c["D"], c["hid"], c["V"], c["max_seq"],
+                                  max_batch=rows)
+    d = {k: np.ascontiguousarray(v) for k, v in w.items() if k != "cfg"}
+    d["emb"] = w["emb"].view(np.uint16)
+    dec.set_weights(d)
+    return w, dec
+
+
+@pytest.mark.parametrize("rows,T", [(4, 2048), (8, 8192)])
+def test_int8_step_multi_split_attention_vs_oracle(gpu, oracle, rows, T):
+    """C3 model dims (16 heads x 128), 2 layers, 4 rows at T 2048 and 8 rows at
+    T 8192: the step's attention runs >= 8 splits (16 at T 8192: past the
+    merge kernel's first batch of 8), merged and quantised per row by
+    pa_merge_row_kernel."""
+    from oracle.oracle import OracleDecoder
+    w, dec = _int8_decoder(oracle, 2, 16, 128, 512, T + 8, rows, seed=51)
+    taps = _Taps(dec, w["cfg"], rows)
+    dec.begin_synthetic(rows, T, 77, True)
+    ns, form = dec.attention_plan()
+    assert form == FORM_SPLIT_MERGE_ROW and ns >= 8, (ns, form)
+    odec = OracleDecoder(oracle, w, rows)
+    decoder_kv_to_oracle(dec, odec, rows, T)
+    flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=T)
+    assert flips < 1e-3 * vals, (flips, vals)
+    print(f"INT8 rows {rows} T {T}: {ns} splits, attention int8 flips {flips}/{vals}, "
+          f"logits rel err {worst:.2e}")
+
+
+def test_int8_c4_beam_state_attention_vs_oracle(gpu, oracle):
+    """The C4 bench state (begin_beams(8, 4, 3840, 256): 240 shared tiles per
+    sequence through page-table forks, 16 private per beam) at C3 head dims,
+    2 layers: the beam-group launch with cost-balanced splits, merged and
+    quantised by pa_merge_row_kernel, against the oracle on every row."""
+    from oracle.oracle import OracleDecoder
+    rows, T = 32, 4096
+    w, dec = _int8_decoder(oracle, 2, 16, 128, 512, T + 8, rows, seed=52)
+    taps = _Taps(dec, w["cfg"], rows)
+    dec.begin_beams(8, 4, 3840, 256, 99, True)
+    ns, form = dec.attention_plan()
+    assert form == (FORM_SPLIT_MERGE_ROW | FORM_BEAM) and ns >= 8, (ns, form)
+    odec = OracleDecoder(oracle, w, rows)
+    distinct = decoder_kv_to_oracle(dec, odec, rows, T)
+    # shared prefixes are read from shared pages: 8 x 16 x 240 + 32 x 16 x 16
+    assert distinct[0] == 8 * 16 * 240 + 32 * 16 * 16, distinct
+    flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=4)
+    assert flips < 1e-3 * vals, (flips, vals)
+    print(f"C4 state: {ns} splits, attention int8 flips {flips}/{vals}, logits {worst:.2e}")
+
+
+def test_f16_step_workgroup_merge_vs_oracle(gpu, oracle):
+    """C2 dims (12 heads x 64, 16 rows, T 2048): the FP16 decoder's attention
+    merges its splits inside the split workgroup (3 splits) and writes the
+    packed fp16 o_proj input, compared with the oracle's fp32 attention."""
+    torch = _torch()
+    import llm_decoder
+    from oracle.oracle import OracleDecoder
+    rows, T, L, H, D, V = 16, 2048, 2, 12, 64, 512
+    rng = np.random.default_rng(61)
+    hid, inter = H * D, 4 * H * D
+    w = {"cfg": dict(L=L, H=H, D=D, hid=hid, inter=inter, V=V, max_seq=T + 8)}
+    w["emb"] = rng.standard_normal((V, hid)).astype(np.float16)
+    for k in ("ln1_g", "ln2_g"):
+        w[k] = (1 + 0.1 * rng.standard_normal((L, hid))).astype(np.float32)
+    for k in ("ln1_b", "ln2_b"):
+        w[k] = (0.1 * rng.standard_normal((L, hid))).astype(np.float32)
+    for k, shp in (("wqkv", (hid, 3 * hid)), ("wo", (hid, hid)), ("w1", (hid, inter)),
+                   ("w2", (inter, hid))):
+        w[k] = (0.02 * rng.standard_normal((L,) + shp)).astype(np.float16)
+    w["b1"] = (0.02 * rng.standard_normal((L, inter))).astype(np.float32)
+    w["b2"] = (0.02 * rng.standard_normal((L, hid))).astype(np.float32)
+    dec = llm_decoder.CUDADecoder(L, H, D, hid, V, T + 8, max_batch=rows)
+    d = {k: np.ascontiguousarray(v) for k, v in w.items() if k != "cfg"}
+    for k in ("emb", "wqkv", "wo", "w1", "w2"):
+        d[k] = d[k].view(np.uint16)
+    dec.set_weights(d)
+    taps = _Taps(dec, w["cfg"], rows, f16=True)
+    dec.begin_synthetic(rows, T, 5, True)
+    ns, form = dec.attention_plan()
+    assert form == FORM_WG_MERGE and 2 <= ns <= 8, (ns, form)
+    odec = OracleDecoder(oracle, w, rows)
+    decoder_kv_to_oracle(dec, odec, rows, T)
+    logits = torch.empty((rows, V), device="cuda")
+    tok = [int(t) for t in rng.integers(0, V, rows)]
+    ulp_flips = 0
+    for s in range(2):
+        g_next = dec.step(tok, logits_ptr=logits.data_ptr())
+        torch.cuda.synchronize()
+        o_logits, o_next, _, attn = odec.step_attn(np.array(tok, np.int32),
+                                                   np.full(rows, T + s, np.int32))
+        ga = taps.read_attn_f16(rows).astype(np.float32)
+        assert_parity(ga, attn, 1e-3, what=f"step {s} attention rows")
+        # against the oracle's own fp16 rounding: equal, or one fp16 ulp apart
+        oa16 = attn.astype(np.float16)
+        d16 = np.abs(ga.astype(np.float16).view(np.int16).astype(np.int32) -
+                     oa16.view(np.int16).astype(np.int32))
+        assert d16[np.sign(ga) == np.sign(oa16)].max() <= 1
+        ulp_flips += int((d16 != 0).sum())
+        gl = logits.cpu().numpy()
+        assert_parity(gl, o_logits, LOGIT_TOL, axis=1, what=f"step {s} logits")
+        _check_tokens(g_next, o_next, o_logits)
+        tok = list(g_next)
+    assert ulp_flips < 1e-3 * 2 * L * rows * hid, ulp_flips
+    print(f"FP16 C2 dims: {ns} splits (workgroup merge), fp16 ulp flips {ulp_flips}")

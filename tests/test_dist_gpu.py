@@ -1,0 +1,122 @@
+"""The multi-GPU decode loop on the GPU: two gloo ranks, both on cuda:0, each
+running bench.py's loop (dist_decode.ShardedDecode + timed_run) over its own
+HIP INT8Decoder (HipDecoderStep), staging every step's output through host
+memory for the gloo gather.  Weak sharding (3 rows per rank) and ragged
+strong sharding (5 rows over 2 ranks), logits and greedy-id gathers.  Rank
+0's gathered steps must equal ONE process stepping all rows, bit for bit.
+
+The model's context stays below one attention split (max_seq 48: every launch
+is the direct single-split form at any row count) and its LayerNorms run in
+the GEMM prologue at every row count, so a row's results do not depend on how
+many rows share its decoder; the weight GEMMs' int32 sums are exact in every
+tile form.  On the 8-GPU node the same loop runs one rank per GPU over RCCL
+(bench.py --gpus N); this test keeps the driver's GPU run exercising it."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"
+WARMUP, STEPS, ROWS_PER_RANK, V = 2, 4, 3, 300
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _decoder(rows):
+    import llm_decoder
+    from oracle.oracle import Oracle, synthetic_int8_model
+    w = synthetic_int8_model(Oracle(), L=2, H=4, D=64, V=V, max_seq=48, seed=23)
+    c = w["cfg"]
+    dec = llm_decoder.INT8Decoder(c["L"], c["H"], c["D"], c["hid"], c["V"], c["max_seq"],
+                                  max_batch=rows)
+    d = {k: np.ascontiguousarray(v) for k, v in w.items() if k != "cfg"}
+    d["emb"] = w["emb"].view(np.uint16)
+    dec.set_weights(d)
+    dec.begin_synthetic(rows, 0, 0, False)
+    return dec
+
+
+def _tokens(mode, world, rank, global_rows):
+    from dist_decode import shard_range
+    if mode == "weak":
+        return np.random.default_rng(1234 + rank).integers(0, V, ROWS_PER_RANK).astype(np.int32)
+    lo, hi = shard_range(global_rows, world, rank)
+    return np.random.default_rng(1234).integers(0, V, global_rows).astype(np.int32)[lo:hi]
+
+
+def _run(rows, world, rank, shard_rows, gather, first):
+    import dist_decode
+    dec = _decoder(rows)
+    sd = dist_decode.ShardedDecode(dist_decode.HipDecoderStep(dec), rows, V, world=world,
+                                   rank=rank, shard_rows=shard_rows, gather=gather,
+                                   staging="host", keep=True)
+    elapsed = dist_decode.timed_run(sd, WARMUP, STEPS, [int(t) for t in first],
+                                    timer_device="cpu")
+    return [t.numpy().copy() for t in sd.finish()], elapsed
+
+
+def _worker(rank, world, port, mode, gather, global_rows, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (str(ROOT), str(PKG)):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import dist_decode
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard_rows = None
+    if mode == "weak":
+        rows = ROWS_PER_RANK
+    else:
+        shard_rows = dist_decode.shard_sizes(global_rows, world)
+        rows = shard_rows[rank]
+    collected, elapsed = _run(rows, world, rank, shard_rows, gather,
+                              _tokens(mode, world, rank, global_rows))
+    if rank == 0:
+        q.put((collected, elapsed))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,gather,global_rows", [
+    ("weak", "logits", 0),
+    ("weak", "ids", 0),
+    ("strong", "logits", 5),  # ragged: 3 + 2, point-to-point receives on rank 0
+    ("strong", "ids", 5),
+])
+def test_sharded_hip_decode_matches_one_process(gpu, mode, gather, global_rows):
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, gather, global_rows, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        collected, elapsed = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert elapsed > 0 and len(collected) == WARMUP + STEPS
+    first = np.concatenate([_tokens(mode, world, r, global_rows) for r in range(world)])
+    ref, _ = _run(len(first), 1, 0, None, gather, first)
+    for s in range(WARMUP + STEPS):
+        assert collected[s].shape == ref[s].shape, (s, collected[s].shape, ref[s].shape)
+        assert np.array_equal(collected[s].view(np.uint32) if gather == "logits" else collected[s],
+                              ref[s].view(np.uint32) if gather == "logits" else ref[s]), s

@@ -7,7 +7,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from _util import rel_err
+from _util import assert_parity, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -123,7 +123,7 @@ def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
                              beam_ids=torch.from_numpy(beam_ids).cuda()).cpu().numpy()
     ref = oracle.paged_attention(q, kpool.float().cpu().numpy(), vpool.float().cpu().numpy(),
                                  table.cpu().numpy(), T=T, beam_ids=beam_ids)
-    assert rel_err(out, ref) < 1e-3
+    assert_parity(out, ref, 1e-3)
     # beam-aware schedule (rows in groups of 2 and 4): group 2 is bitwise the
     # plain schedule; group 4 may place its split boundaries by cost (shared
     # prefix vs private tail), which changes only the fp32 merge rounding
@@ -197,7 +197,7 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle, D, ts, missing):
                                      context_lens=lens)
         plain = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T,
                                    context_lens=d(lens)).cpu().numpy()
-        assert rel_err(plain, ref) < 1e-3
+        assert_parity(plain, ref, 1e-3)
         for g in (2, 4):
             outg = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
                                       row_group=g).cpu().numpy()
@@ -207,7 +207,7 @@ def test_grouped_attention_shared_prefix_random(gpu, oracle, D, ts, missing):
                 np.testing.assert_array_equal(outg, plain)
             else:
                 assert rel_err(outg, plain) < 1e-5
-            assert rel_err(outg, ref) < 1e-3
+            assert_parity(outg, ref, 1e-3)
 
 
 @pytest.mark.parametrize("shared", [0, 1, 17, 43, 44])
@@ -250,8 +250,8 @@ def test_grouped_attention_cost_balanced_splits(gpu, oracle, shared, T, kvt):
     outg = llm_capi.pa_decode(d(q), kd, vd, d(pt), T=T, row_group=4).cpu().numpy()
     if kvt == "bfloat16":
         np.testing.assert_array_equal(outg, plain)
-    assert rel_err(plain, ref) < 1e-3
-    assert rel_err(outg, ref) < 1e-3
+    assert_parity(plain, ref, 1e-3)
+    assert_parity(outg, ref, 1e-3)
     assert rel_err(outg, plain) < 1e-5
     # fixed pages per split keep the uniform partition, empty splits included
     outf = llm_capi.pa_decode(d(q), kd, vd, d(pt), T=T, row_group=4,
@@ -311,7 +311,7 @@ def test_typed_kv_cache_attention_and_save_load(gpu, oracle, tmp_path, dtype):
                 kpool[pt[b, h, t // TS], t % TS] = ks[b][t, h]
                 vpool[pt[b, h, t // TS], t % TS] = vs[b][t, h]
     ref = oracle.paged_attention(q, kpool, vpool, pt, T=T)
-    assert rel_err(out.cpu().numpy(), ref) < 1e-3
+    assert_parity(out.cpu().numpy(), ref, 1e-3)
     path = str(tmp_path / "kv.bin")
     kv.save_to_file(path, format="snapshot")
     kv2 = llm_decoder.KVTileCache()

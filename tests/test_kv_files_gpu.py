@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import kv_formats
-from _util import GOLDEN, rel_err
+from _util import assert_parity, GOLDEN, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -124,7 +124,7 @@ def test_attention_over_reference_tile_files(gpu, oracle, tmp_path):
         pt[b, h, t] = i
         kpool[i], vpool[i] = kt[b, h, t], vt[b, h, t]
     ref = oracle.paged_attention(q, kpool, vpool, pt, T=T)
-    assert rel_err(out.cpu().numpy(), ref) < 1e-3
+    assert_parity(out.cpu().numpy(), ref, 1e-3)
 
 
 def test_tile_load_semantics_cow_duplicates_and_refusals(gpu, tmp_path):
@@ -229,3 +229,45 @@ def test_corrupt_snapshot_leaves_cache_unchanged(gpu, tmp_path):
     dest.load_from_file(str(snap), format="snapshot")
     assert [dest.lookup(b, 0, t) for b in range(2) for t in range(4)] == \
         [kv.lookup(b, 0, t) for b in range(2) for t in range(4)]
+
+
+def test_tile_load_out_of_pages_leaves_cache_unchanged(gpu, tmp_path):
+    """A record file that needs more free pages (new tiles plus copy-on-write
+    copies of forked ones) than the pool has is refused before any page is
+    allocated: the page table and the free count stay as they were."""
+    ts, D = 16, 64
+    rng = np.random.default_rng(8)
+    kv = _cache(ts, D, np.float16, beams=4, H=2, max_tiles=6, pages=12)
+    base = [((0, h, t), rng.standard_normal((ts, D)).astype(np.float16))
+            for h in range(2) for t in range(3)]
+    (tmp_path / "base.bin").write_bytes(kv_formats.write_tiles(base))
+    kv.load_tiles(str(tmp_path / "base.bin"), "k")
+    kv.fork(0, 1)  # 6 shared pages
+    assert kv.free_pages() == 6
+    before = [kv.lookup(b, h, t) for b in range(4) for h in range(2) for t in range(6)]
+    # 4 copies-on-write of beam 1's shared tiles + 3 new tiles = 7 > 6 free
+    recs = [((1, h, t), rng.standard_normal((ts, D)).astype(np.float16))
+            for h in range(2) for t in range(2)]
+    recs += [((2, 0, t), rng.standard_normal((ts, D)).astype(np.float16)) for t in range(3)]
+    (tmp_path / "big.bin").write_bytes(kv_formats.write_tiles(recs))
+    with pytest.raises(RuntimeError, match="free pages"):
+        kv.load_tiles(str(tmp_path / "big.bin"), "k")
+    assert [kv.lookup(b, h, t) for b in range(4) for h in range(2) for t in range(6)] == before
+    assert kv.free_pages() == 6
+    # one record fewer fits exactly (6 pages) and loads
+    (tmp_path / "fit.bin").write_bytes(kv_formats.write_tiles(recs[:-1]))
+    kv.load_tiles(str(tmp_path / "fit.bin"), "k")
+    assert kv.free_pages() == 0 and kv.lookup(1, 0, 0) != kv.lookup(0, 0, 0)
+
+
+def test_pool_load_of_a_snapshot_names_the_format(gpu, tmp_path):
+    """load_from_file's default format is the reference's pool dump; given a
+    page-table snapshot (the round-1 default) it says so instead of failing on
+    the size alone."""
+    ts, D = 16, 64
+    kv = _cache(ts, D, np.float16, beams=2, H=2, max_tiles=4, pages=20)
+    snap = tmp_path / "snap.bin"
+    kv.save_to_file(str(snap), format="snapshot")
+    with pytest.raises(RuntimeError, match="format='snapshot'"):
+        kv.load_from_file(str(snap))
+    kv.load_from_file(str(snap), format="snapshot")

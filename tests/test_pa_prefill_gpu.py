@@ -10,7 +10,7 @@ pa_decode: 1e-3 relative (max-abs error / max-abs reference)."""
 import numpy as np
 import pytest
 
-from _util import rel_err
+from _util import assert_parity, rel_err
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-3
@@ -75,12 +75,12 @@ def test_pa_prefill_vs_oracle(gpu, oracle, H, D, ts, p0, m, row, split):
                               split=split).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, row, p0)
     assert np.isfinite(out).all()
-    assert rel_err(out, ref) < RTOL, rel_err(out, ref)
+    assert_parity(out, ref, RTOL)
     # and the decode kernel on the same rows agrees
     dec = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=p0 + m,
                              beam_ids=_dev(np.full(m, row, np.int32)),
                              context_lens=_dev(np.arange(p0 + 1, p0 + m + 1, dtype=np.int32)))
-    assert rel_err(out, dec.cpu().numpy()) < RTOL
+    assert_parity(out, dec.cpu().numpy(), RTOL)
 
 
 def test_pa_prefill_missing_pages_and_scale(gpu, oracle):
@@ -93,7 +93,7 @@ def test_pa_prefill_missing_pages_and_scale(gpu, oracle):
     out = llm_capi.pa_prefill(_dev(q), _dev(kp), _dev(vp), _dev(pt), row=1, p0=p0,
                               sm_scale=0.5).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, 1, p0, sm_scale=0.5)
-    assert rel_err(out, ref) < RTOL, rel_err(out, ref)
+    assert_parity(out, ref, RTOL)
 
 
 def test_pa_prefill_all_missing_is_zero(gpu):
@@ -122,7 +122,7 @@ def test_pa_prefill_strided_q_interleaved_pools(gpu, oracle):
     wide[:, :H * D] = _dev(q.reshape(m, H * D))
     out = llm_capi.pa_prefill(wide, kv[:, 0], kv[:, 1], _dev(pt), row=0, p0=p0).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, 0, p0)
-    assert rel_err(out, ref) < RTOL
+    assert_parity(out, ref, RTOL)
 
 
 def test_pa_prefill_rejects_unsupported(gpu):

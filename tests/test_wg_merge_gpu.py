@@ -46,7 +46,7 @@ def _model(rng, L, H, D, V):
     return {k: np.ascontiguousarray(v) for k, v in w.items()}
 
 
-def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0):
+def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16):
     """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`
     (tuning build: splits > 0 forces the split count)."""
     import torch
@@ -62,7 +62,7 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0):
     lib.llm_decoder_sync.argtypes = [ctypes.c_void_p]
     lib.llm_decoder_destroy.argtypes = [ctypes.c_void_p]
     lib.llm_decoder_destroy.restype = None
-    cfg = _Cfg(L, H, D, H * D, V, S, 0, 16, llm_capi.LLM_F16, B, 1.0, 0)
+    cfg = _Cfg(L, H, D, H * D, V, S, 0, ts, llm_capi.LLM_F16, B, 1.0, 0)
     dec = ctypes.c_void_p()
     llm_capi.check(lib.llm_decoder_create(ctypes.byref(cfg), ctypes.byref(dec)), lib)
     try:
@@ -86,20 +86,25 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0):
         os.environ.pop("LLM_WGM_SPLITS", None)
 
 
+@pytest.mark.parametrize("H,D,ts", [(12, 64, 16), (8, 128, 16), (4, 256, 16), (8, 128, 32)],
+                         ids=["c2_width_d64", "d128", "d256", "d128_page32"])
 @pytest.mark.parametrize("ctx", [1500, 40])
-def test_wg_merge_bitwise_c2_width(gpu, ctx):
+def test_wg_merge_bitwise(gpu, ctx, H, D, ts):
     """Same split count, with and without the workgroup merge: same bits (at
-    ctx 40 = 3 tiles, 5 splits leave two empty); and the product build's own
-    split choice equals the tuning build's."""
+    ctx 40, 5 and 8 splits leave splits past the row's tiles empty); and the
+    product build's own split choice equals the tuning build's.  C2's width
+    (12 x 64) and the other head dims the FP16 decoder runs the merge form at
+    (D 128 and 256, page 32), whose 512-thread workgroups halve the register
+    budget of the 2-stage register staging."""
     import llm_capi
     tune = llm_capi.load_tune()
-    L, H, D, V, S, B = 2, 12, 64, 512, 2100, 16
+    L, V, S, B = 2, 512, 2100, 16
     w = _model(np.random.default_rng(3), L, H, D, V)
-    for ns in (3, 5, 8):
-        on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, ns)
-        off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False, ns)
+    for ns in ((3, 5, 8) if D == 64 else (3, 8)):
+        on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, ns, ts)
+        off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False, ns, ts)
         assert np.isfinite(on).all()
         assert np.array_equal(on.view(np.uint32), off.view(np.uint32)), (ns, np.abs(on - off).max())
-    auto = _run(tune, w, L, H, D, V, S, B, ctx, 3, True)
-    prod = _run(llm_capi.load(), w, L, H, D, V, S, B, ctx, 3, True)
+    auto = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, 0, ts)
+    prod = _run(llm_capi.load(), w, L, H, D, V, S, B, ctx, 3, True, 0, ts)
     assert np.array_equal(prod.view(np.uint32), auto.view(np.uint32))
