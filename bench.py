@@ -330,6 +330,10 @@ def main():
     backend = os.environ.get("LLM_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    # every step, staging copy, gather and timing event runs on ONE explicit
+    # stream (torch's default stream has handle 0, which the C ABI reads as the
+    # decoder's own non-blocking stream)
+    torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

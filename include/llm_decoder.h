@@ -440,9 +440,9 @@ int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* stream);
  *                                                           inter_dim at s = 3;
  *   slot stride ceil(max_batch/16)*16 * max(hidden_dim, inter_dim) bytes)
  * and their fp32 dequantisation scales to s_dev[(l*4 + s) * max_batch + row].
- * FP16 decoders (CUDADecoder) tap stage 1 only -- the merged attention rows as
- * the fp16 o_proj input, packed-A order (a_frag_off_f16), at the same slot
- * layout with 2 bytes per element; s_dev is not written.
+ * FP16 decoders (CUDADecoder) tap their four fp16 GEMM inputs in packed-A
+ * order (a_frag_off_f16), at the same slot layout with 2 bytes per element;
+ * s_dev is not written (give any device buffer).
  * Both NULL switches the taps off.  Prefill chunks are not tapped. */
 int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev);
 /* The attention launch of the decoder's step at its current batch and row

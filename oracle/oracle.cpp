@@ -447,10 +447,16 @@ uint16_t* oracle_decoder_kv_ptr(void* h, int layer, int which) {
 // attn_out (optional, [L][B][hid] fp32): every layer's attention output before
 // the o_proj input conversion (int8 quantisation or the fp16 rounding of the
 // CUDADecoder), for checks of the GPU's merged attention rows.
+// forced_kv (optional, fp16 bits [L][B][2][H][D]): the K and V the step
+// appends at pos, taken instead of the oracle's own fp16 rounding of its
+// projection (the fp16 decoder's GEMM accumulates in another fp32 order, so a
+// value can round one ulp apart); kv_stats [L][2]: values that differed, max
+// |difference| / (one fp16 ulp + 1e-6 of the head's largest value).
 static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
                         int32_t* next_out, const int8_t* forced_q, const float* forced_s,
-                        float* stats, float* attn_out);
+                        float* stats, float* attn_out, const uint16_t* forced_kv = nullptr,
+                        float* kv_stats = nullptr);
 
 int oracle_decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
@@ -467,19 +473,25 @@ int oracle_decoder_step_forced(void* handle, const int32_t* tokens, const int32_
 }
 
 // oracle_decoder_step / _step_forced with the per-layer attention outputs
-// (forced_q NULL: a free step; the fp16 CUDADecoder restatement takes no forcing)
+// (forced_q NULL: a free step).  The fp16 CUDADecoder restatement is forced at
+// its four fp16 GEMM inputs instead: forced_q then points to fp16 bits
+// [L][4][B][Kmax] (uint16), forced_s is unused, and stats hold per (layer,
+// stage): the fp16 values that differ from the oracle's own rounding, the max
+// of |difference| / (one fp16 ulp of the value + 1e-6 of the row's largest
+// value) -- <= 1 is a rounding flip --, and the max |difference| / row max.
 int oracle_decoder_step_attn(void* handle, const int32_t* tokens, const int32_t* pos,
                              float attn_scale, float* logits_out, int32_t* next_out,
                              const int8_t* forced_q, const float* forced_s, float* stats,
-                             float* attn_out) {
+                             float* attn_out, const uint16_t* forced_kv, float* kv_stats) {
   return decoder_step(handle, tokens, pos, attn_scale, -1, 1, nullptr, logits_out, next_out,
-                      forced_q, forced_s, stats, attn_out);
+                      forced_q, forced_s, stats, attn_out, forced_kv, kv_stats);
 }
 
 static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos, float attn_scale,
                         int layers_to_run, int do_lm_head, float* x_out, float* logits_out,
                         int32_t* next_out, const int8_t* forced_q, const float* forced_s,
-                        float* stats, float* attn_out) {
+                        float* stats, float* attn_out, const uint16_t* forced_kv,
+                        float* kv_stats) {
   auto* d = static_cast<OracleDecoder*>(handle);
   const oracle_model& m = d->m;
   const int B = d->B, H = m.H, D = m.D, hid = m.hid, inter = m.inter;
@@ -487,7 +499,6 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
     if (pos[b] < 0 || pos[b] >= m.max_seq || tokens[b] < 0 || tokens[b] >= m.V) return 2;
   const int Lrun = layers_to_run < 0 ? m.L : std::min(layers_to_run, m.L);
   const bool f16w = m.hwqkv != nullptr;
-  if (f16w && forced_q) return 3;  // teacher forcing is for the int8 activations
   std::vector<float> x((size_t)B * hid), a((size_t)B * hid), qkv((size_t)B * 3 * hid),
       o((size_t)B * hid), h1((size_t)B * inter);
   std::vector<int8_t> qa((size_t)B * std::max(hid, inter));
@@ -520,10 +531,43 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
       stats[slot * 3 + 2] = max_srel;
     }
   };
+  // fp16 decoder: round `in` [B][K] to fp16 as the GEMM consumes it, then
+  // (teacher forcing) compare with and take the given fp16 activations
+  auto force16 = [&](int l, int stage, float* in, int K) {
+    if (!forced_q) return;
+    const uint16_t* fh = reinterpret_cast<const uint16_t*>(forced_q);
+    const size_t slot = (size_t)l * 4 + stage;
+    float n_diff = 0, max_ratio = 0, max_abs = 0;
+    for (int b = 0; b < B; ++b) {
+      const uint16_t* f = fh + (slot * B + b) * Kmax;
+      float* row = in + (size_t)b * K;
+      float rmax = 0.f;
+      for (int j = 0; j < K; ++j) rmax = std::max(rmax, std::fabs(row[j]));
+      for (int j = 0; j < K; ++j) {
+        const uint16_t own = float_to_half(row[j]);
+        if (own != f[j]) {
+          n_diff += 1;
+          // one fp16 ulp (2^-10 relative) of the value, or 1e-6 of the row's
+          // largest value for values near zero (subnormal ulps are tiny)
+          const float d = std::fabs(half_to_float(own) - half_to_float(f[j]));
+          const float tol = std::ldexp(std::fabs(half_to_float(own)), -10) + 1e-6f * rmax;
+          max_ratio = std::max(max_ratio, d / std::max(tol, 1e-30f));
+          max_abs = std::max(max_abs, d / std::max(rmax, 1e-30f));
+        }
+        row[j] = half_to_float(f[j]);
+      }
+    }
+    if (stats) {
+      stats[slot * 3 + 0] = n_diff;
+      stats[slot * 3 + 1] = max_ratio;
+      stats[slot * 3 + 2] = max_abs;
+    }
+  };
   for (int l = 0; l < Lrun; ++l) {
     const size_t lh = (size_t)l * hid;
     oracle_layer_norm(x.data(), B, hid, m.ln1_g + lh, m.ln1_b + lh, 1e-5f, a.data());
     if (f16w) {
+      force16(l, 0, a.data(), hid);
       f16_gemm(a.data(), B, hid, m.hwqkv + (size_t)l * hid * 3 * hid, 3 * hid, nullptr, 0,
                qkv.data());
     } else {
@@ -531,14 +575,33 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
       oracle_i8_gemm(qa.data(), m.wqkv + (size_t)l * hid * 3 * hid, nullptr, qkv.data(), B,
                      3 * hid, hid, sa.data(), m.sw_qkv + (size_t)l * 3 * hid, nullptr, 0);
     }
-    // KV append (fp16 storage, round to nearest even).
+    // KV append (fp16 storage, round to nearest even), or the forced K / V
+    float kv_nd = 0.f, kv_ratio = 0.f;
     for (int b = 0; b < B; ++b)
       for (int hh = 0; hh < H; ++hh)
-        for (int dd = 0; dd < D; ++dd) {
-          const size_t idx = d->kv_index(l, b, hh, pos[b]) + dd;
-          d->k[idx] = float_to_half(qkv[(size_t)b * 3 * hid + hid + hh * D + dd]);
-          d->v[idx] = float_to_half(qkv[(size_t)b * 3 * hid + 2 * hid + hh * D + dd]);
+        for (int which = 0; which < 2; ++which) {
+          const float* src = qkv.data() + (size_t)b * 3 * hid + (1 + which) * hid + hh * D;
+          uint16_t* dst = (which ? d->v.data() : d->k.data()) + d->kv_index(l, b, hh, pos[b]);
+          const uint16_t* f =
+              forced_kv ? forced_kv + ((((size_t)l * B + b) * 2 + which) * H + hh) * D : nullptr;
+          float hmax = 0.f;
+          if (f)
+            for (int dd = 0; dd < D; ++dd) hmax = std::max(hmax, std::fabs(src[dd]));
+          for (int dd = 0; dd < D; ++dd) {
+            const uint16_t own = float_to_half(src[dd]);
+            dst[dd] = own;
+            if (!f || f[dd] == own) continue;
+            kv_nd += 1.f;
+            const float diff = std::fabs(half_to_float(own) - half_to_float(f[dd]));
+            const float tol = std::ldexp(std::fabs(half_to_float(own)), -10) + 1e-6f * hmax;
+            kv_ratio = std::max(kv_ratio, diff / std::max(tol, 1e-30f));
+            dst[dd] = f[dd];
+          }
         }
+    if (kv_stats) {
+      kv_stats[2 * l] = kv_nd;
+      kv_stats[2 * l + 1] = kv_ratio;
+    }
     // Attention: the reference scores are dot/temperature and its softmax divides
     // by temperature again (Appendix A #13); attn_scale = 1/temperature^2 folds
     // both.  exp(s - max) / (sum + 1e-6), out = sum p v.
@@ -568,10 +631,13 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
     }
     if (attn_out) std::memcpy(attn_out + (size_t)l * B * hid, o.data(), sizeof(float) * B * hid);
     if (f16w) {
+      force16(l, 1, o.data(), hid);
       f16_gemm(o.data(), B, hid, m.hwo + (size_t)l * hid * hid, hid, nullptr, 0, x.data());
       oracle_layer_norm(x.data(), B, hid, m.ln2_g + lh, m.ln2_b + lh, 1e-5f, a.data());
+      force16(l, 2, a.data(), hid);
       f16_gemm(a.data(), B, hid, m.hw1 + (size_t)l * hid * inter, inter,
                m.b1 + (size_t)l * inter, 1, h1.data());
+      force16(l, 3, h1.data(), inter);
       f16_gemm(h1.data(), B, inter, m.hw2 + (size_t)l * inter * hid, hid, m.b2 + lh, 0, x.data());
       continue;
     }

@@ -127,7 +127,8 @@ class Oracle:
                                                  _f32p, _i32p, _i8p, _f32p, _f32p]
         L.oracle_decoder_step_attn.restype = ctypes.c_int
         L.oracle_decoder_step_attn.argtypes = [ctypes.c_void_p, _i32p, _i32p, ctypes.c_float,
-                                               _f32p, _i32p, _i8p, _f32p, _f32p, _f32p]
+                                               _f32p, _i32p, _i8p, _f32p, _f32p, _f32p, _u16p,
+                                               _f32p]
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_set_num_threads.argtypes = [ctypes.c_int]
 
@@ -285,11 +286,19 @@ class OracleDecoder:
         assert rc == 0, rc
         return logits, nxt, stats
 
-    def step_attn(self, tokens, pos, forced_q=None, forced_s=None, attn_scale=1.0):
-        """A step (teacher-forced when forced_q / forced_s are given, INT8
-        weights only) that also returns every layer's attention output before
-        the o_proj input conversion: (logits, next, stats or None, attn
-        [L][B][hid] fp32)."""
+    def step_attn(self, tokens, pos, forced_q=None, forced_s=None, attn_scale=1.0,
+                  forced_kv=None):
+        """A step that also returns every layer's attention output before the
+        o_proj input conversion: (logits, next, stats or None, attn [L][B][hid]
+        fp32).  Teacher forced when forced_q is given: int8 [L][4][B][Kmax] +
+        forced_s scales for INT8 weights, or fp16 [L][4][B][Kmax] (float16 /
+        uint16 bits, forced_s unused) for the fp16 CUDADecoder restatement,
+        whose stats are (fp16 values that differ, max |difference| / (one
+        fp16 ulp + 1e-6 of the row's max), max |difference| / row max).
+        forced_kv (fp16 [L][B][2][H][D]): the K / V the step appends, taken
+        instead of the oracle's own rounding; self.kv_stats [L][2] then holds
+        (values that differed, max |difference| / (one ulp + 1e-6 of the head's
+        max))."""
         c = self.cfg
         tokens = np.ascontiguousarray(tokens, np.int32)
         pos = np.ascontiguousarray(pos, np.int32)
@@ -298,15 +307,26 @@ class OracleDecoder:
         attn = np.empty((c["L"], self.B, c["hid"]), np.float32)
         stats = fq = fs = None
         if forced_q is not None:
-            fq = np.ascontiguousarray(forced_q, np.int8)
-            fs = np.ascontiguousarray(forced_s, np.float32)
-            assert fq.shape == (c["L"], 4, self.B, max(c["hid"], c["inter"])), fq.shape
-            assert fs.shape == (c["L"], 4, self.B), fs.shape
+            shape = (c["L"], 4, self.B, max(c["hid"], c["inter"]))
+            if np.asarray(forced_q).dtype in (np.float16, np.uint16):
+                fq = np.ascontiguousarray(np.asarray(forced_q).view(np.uint16)).view(np.int8)
+                assert fq.shape[:3] == shape[:3] and fq.shape[3] == 2 * shape[3], fq.shape
+            else:
+                fq = np.ascontiguousarray(forced_q, np.int8)
+                fs = np.ascontiguousarray(forced_s, np.float32)
+                assert fq.shape == shape, fq.shape
+                assert fs.shape == (c["L"], 4, self.B), fs.shape
             stats = np.zeros((c["L"], 4, 3), np.float32)
+        fkv = None
+        self.kv_stats = None
+        if forced_kv is not None:
+            fkv = np.ascontiguousarray(np.asarray(forced_kv).view(np.uint16))
+            assert fkv.shape == (c["L"], self.B, 2, c["H"], c["D"]), fkv.shape
+            self.kv_stats = np.zeros((c["L"], 2), np.float32)
         rc = self.o.lib.oracle_decoder_step_attn(
             self.h, _ptr(tokens, _i32p), _ptr(pos, _i32p), attn_scale, _ptr(logits, _f32p),
             _ptr(nxt, _i32p), _ptr(fq, _i8p), _ptr(fs, _f32p), _ptr(stats, _f32p),
-            _ptr(attn, _f32p))
+            _ptr(attn, _f32p), _ptr(fkv, _u16p), _ptr(self.kv_stats, _f32p))
         assert rc == 0, rc
         return logits, nxt, stats, attn
 

@@ -477,15 +477,14 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
     g.C16 = R.act2;
   }
   RET_IF(weight_gemm(g, st));
-  if (i8) RET_IF(tap(l, 2, R, hid, st));
+  RET_IF(tap(l, 2, R, hid, st));
   g.ln_x = nullptr; g.ln_emb = nullptr; g.act_out = nullptr; g.sa_out = nullptr;
   g.C16 = nullptr;
   if (!i8) g.A = R.act2;
   // quantise h1 -> mlp_fc2 (+b2)
-  if (i8) {
+  if (i8)
     LLM_HIP_RET(launch_quantize_rows(R.h1, R.n, inter, static_cast<int8_t*>(R.act), R.sa, st, 1));
-    RET_IF(tap(l, 3, R, inter, st));
-  }
+  RET_IF(tap(l, 3, R, inter, st));
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
@@ -519,17 +518,17 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
 // Tap stage `stage` of layer l (0: LN1 out, 1: attention out, 2: LN2 out,
 // 3: fc1 out): the rows' packed int8 activations (K per row) and row scales.
 // Decode rows only (prefill chunks are not tapped); captured into the graph.
-// FP16 decoders: stage 1 only (the merged attention rows as the packed fp16
-// o_proj input, 2 bytes per element, no scales).
+// FP16 decoders: the four packed fp16 GEMM inputs (2 bytes per element, no
+// scales); stage 3 (fc2's input) is act2, written by the fc1 epilogue.
 int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
   if (!tap_q || R.prefill_row >= 0 || R.beam_rows) return LLM_OK;
   const bool f16 = wdtype == LLM_F16;
-  if (f16 && stage != 1) return LLM_OK;
   const size_t es = f16 ? 2 : 1;
   const size_t slot = (size_t)l * 4 + stage;
   const size_t n16 = ((size_t)R.n + 15) / 16 * 16;
   const size_t r0 = (size_t)R.table_row0;  // rows r0.. of the step (16-row aligned)
-  LLM_HIP_RET(hipMemcpyAsync(tap_q + (slot * b16 * qa_ld + r0 * K) * es, R.act, n16 * K * es,
+  const void* src = f16 && stage == 3 ? R.act2 : R.act;
+  LLM_HIP_RET(hipMemcpyAsync(tap_q + (slot * b16 * qa_ld + r0 * K) * es, src, n16 * K * es,
                              hipMemcpyDeviceToDevice, st));
   if (!f16)
     LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, R.sa, sizeof(float) * R.n,

@@ -119,12 +119,22 @@ class _Works:
 class HipDecoderStep:
     """One decode step of an llm_decoder INT8Decoder / CUDADecoder on a HIP
     stream: logits (if asked) go to a device tensor, greedy ids to an int32
-    device tensor, without a host synchronisation."""
+    device tensor, without a host synchronisation.
+
+    The stream must be the one the caller's torch work (staging copies,
+    gathers, events) is ordered on, and it cannot be torch's default stream:
+    its handle is 0, which the C ABI reads as "the decoder's own stream" (a
+    non-blocking stream that does not synchronise with the default one).  Run
+    under torch.cuda.stream(torch.cuda.Stream()) or pass such a stream."""
 
     def __init__(self, dec, stream=None):
         import torch
         self.dec = dec
         self.sp = (stream or torch.cuda.current_stream()).cuda_stream
+        if not self.sp:
+            raise ValueError("HipDecoderStep needs a non-default torch stream (the C ABI reads "
+                             "stream 0 as the decoder's own stream): run it under "
+                             "torch.cuda.stream(torch.cuda.Stream())")
 
     def __call__(self, tokens, logits_out):
         self.dec.step(tokens, logits_ptr=logits_out.data_ptr() if logits_out is not None else 0,

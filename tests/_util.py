@@ -120,3 +120,31 @@ def decoder_kv_to_oracle(dec, odec, rows, T):
             pages = pool[ids, which]    # [rows][H][nt][ts][D]
             kv[:rows, :, :T] = pages.reshape(rows, H, nt * ts, D)[:, :, :T]
     return distinct
+
+
+def decoder_kv_at(dec, rows, pos, L):
+    """The K and V the decoder's last step appended: fp16 [L][rows][2][H][D] at
+    position pos[r] of each row, read back from its pages (teacher forcing of
+    the fp16 decoder's KV append: OracleDecoder.step_attn(forced_kv=...))."""
+    import ctypes
+    import llm_capi
+    lib = llm_capi.load()
+    kvh = ctypes.c_void_p(dec.kv_handle)
+    view = llm_capi.PaKvView()
+    llm_capi.check(lib.kv_cache_view(kvh, 0, ctypes.byref(view)))
+    ts, D, H, mt = view.page_size, view.head_dim, view.num_heads, view.max_tiles
+    stride = lib.kv_cache_page_stride(kvh)
+    base = lib.kv_cache_k_pool(kvh)
+    out = np.empty((L, rows, 2, H, D), np.float16)
+    page = np.empty((2, ts, D), np.float16)
+    for layer in range(L):
+        pt = np.empty((view.num_beams, H, mt), np.int32)
+        hip_copy_to_host(pt, lib.kv_cache_page_table(kvh, layer))
+        for r in range(rows):
+            p = int(pos[r])
+            for h in range(H):
+                pg = int(pt[r, h, p // ts])
+                assert pg >= 0
+                hip_copy_to_host(page, base + pg * stride)
+                out[layer, r, :, h] = page[:, p % ts]
+    return out

@@ -26,7 +26,7 @@ propagate and are held to FREE_RUN_TOL, a drift bound, not a parity bar."""
 import numpy as np
 import pytest
 
-from _util import assert_parity, decoder_kv_to_oracle, rel_err
+from _util import assert_parity, decoder_kv_at, decoder_kv_to_oracle, rel_err
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
@@ -365,48 +365,92 @@ def _f16_reference_logits(w, tokens_per_step, oracle):
 def test_cuda_decoder_fp16_vs_oracle(gpu, oracle, H, S):
     """CUDADecoder (fp16 weights, fp16 GEMM inputs, fp16 KV) against the
     oracle's restated CUDADecoder step (oracle.cpp f16_gemm path), 24 steps of
-    ragged prompts then fed-back tokens: logits within LOGIT_TOL, tokens exact
-    unless the oracle's top two are within TIE_TOL.  No int8 rounding here, so
-    no teacher forcing is needed (an fp16 rounding flip moves a logit ~1e-6).
-    A float64 numpy restatement (_f16_reference_logits) agrees as well.
-    H 12 is C2's width (hid 768, inter 3072).  S 512 gives the attention 4
-    splits, so it runs in the workgroup-merge form (splits past a short row's
-    tiles empty); S 40 is a single-split launch."""
+    ragged prompts then fed-back tokens, TEACHER FORCED at the four fp16 GEMM
+    inputs (taps) and at the K / V each step appends (read back from the
+    pages): an fp32 reduction-order difference can move an activation
+    across an fp16 rounding boundary (one ulp, 2^-11 relative), which free
+    running lets propagate to ~5e-4 of the logit scale; forced, every step is
+    held to the north_star bar -- logits within LOGIT_TOL tensor-normalised
+    AND elementwise per row, fp16 inputs within one ulp (< 1e-3 differing),
+    tokens exact unless the oracle's top two are within TIE_TOL.  A free-running
+    pass (no taps) is then held to LOGIT_TOL tensor-normalised, and a float64
+    numpy restatement (_f16_reference_logits) to the same.  H 12 is C2's width
+    (hid 768, inter 3072).  S 512 gives the attention 4 splits, so it runs in
+    the workgroup-merge form (splits past a short row's tiles empty); S 40 is a
+    single-split launch."""
     torch = _torch()
     import llm_decoder
-    from oracle.oracle import OracleDecoder
+    from oracle.oracle import OracleDecoder, unpack_a_f16
     rng = np.random.default_rng(9)
     L, D, V = 2, 64, 300
     w = _f16_model(rng, L, H, D, V, S)
     c = w["cfg"]
-    dec = llm_decoder.CUDADecoder(L, H, D, c["hid"], V, S, max_batch=2)
+    hid, inter = c["hid"], c["inter"]
+    dec = llm_decoder.CUDADecoder(L, H, D, hid, V, S, max_batch=2)
     d = {k: np.ascontiguousarray(v) for k, v in w.items() if k != "cfg"}
     for k in ("emb", "wqkv", "wo", "w1", "w2"):
         d[k] = d[k].view(np.uint16)
     dec.set_weights(d)
-    odec = OracleDecoder(oracle, w, 2)
-    dec.begin_synthetic(2, 0, 0, False)
+    Kmax, b16 = max(hid, inter), 16
+    tq = torch.zeros(L * 4 * b16 * Kmax * 2, dtype=torch.int8, device="cuda")
+    ts_ = torch.zeros(L * 4 * 2, dtype=torch.float32, device="cuda")
+    dec.set_taps(tq.data_ptr(), ts_.data_ptr())
+
+    def read_forced():
+        q = tq.cpu().numpy().view(np.uint16).reshape(L, 4, b16 * Kmax)
+        fh = np.zeros((L, 4, 2, Kmax), np.float16)
+        for l in range(L):
+            for st in range(4):
+                Kst = inter if st == 3 else hid
+                fh[l, st, :, :Kst] = unpack_a_f16(q[l, st, :b16 * Kst], 2, Kst)
+        return fh
+
     prompts = [rng.integers(0, V, 7).tolist(), rng.integers(0, V, 2).tolist()]
     logits = torch.empty((2, V), device="cuda")
-    nxt, seen = [0, 0], []
-    for s_ in range(24):
-        tok = [p[s_] if s_ < len(p) else nxt[b] for b, p in enumerate(prompts)]
-        g_next = dec.step(tok, logits_ptr=logits.data_ptr())
-        torch.cuda.synchronize()
-        _, ol, on = odec.step(np.array(tok, np.int32), np.full(2, s_, np.int32))
-        gl = logits.cpu().numpy()
-        assert_parity(gl, ol, LOGIT_TOL, axis=1, what=f"step {s_} logits")
-        for b in range(2):
-            if g_next[b] != on[b]:
-                assert ol[b][on[b]] - ol[b][g_next[b]] <= TIE_TOL * np.abs(ol[b]).max()
-        seen.append(tok)
-        nxt = list(g_next)
+
+    def lockstep(forced):
+        odec = OracleDecoder(oracle, w, 2)
+        dec.begin_synthetic(2, 0, 0, False)
+        nxt, seen, worst, flips = [0, 0], [], 0.0, 0
+        for s_ in range(24):
+            tok = [p[s_] if s_ < len(p) else nxt[b] for b, p in enumerate(prompts)]
+            g_next = dec.step(tok, logits_ptr=logits.data_ptr())
+            torch.cuda.synchronize()
+            if forced:
+                ol, on, stats, _ = odec.step_attn(np.array(tok, np.int32), np.full(2, s_, np.int32),
+                                                  read_forced(),
+                                                  forced_kv=decoder_kv_at(dec, 2, [s_, s_], L))
+                assert stats[:, :, 1].max() <= 1, (s_, stats)
+                assert odec.kv_stats[:, 1].max() <= 1, (s_, odec.kv_stats)
+                flips += int(stats[:, :, 0].sum())
+            else:
+                _, ol, on = odec.step(np.array(tok, np.int32), np.full(2, s_, np.int32))
+            gl = logits.cpu().numpy()
+            worst = max(worst, rel_err(gl, ol))
+            assert rel_err(gl, ol) < LOGIT_TOL, (forced, s_, rel_err(gl, ol))
+            if forced:
+                assert_parity(gl, ol, LOGIT_TOL, axis=1, what=f"step {s_} logits")
+            for b in range(2):
+                if g_next[b] != on[b]:
+                    assert ol[b][on[b]] - ol[b][g_next[b]] <= TIE_TOL * np.abs(ol[b]).max()
+            seen.append(tok)
+            nxt = list(g_next)
+        return seen, worst, flips
+
+    seen, worst, flips = lockstep(True)
+    # an fp16 rounding boundary is 2^-11 of the value apart (int8: 1/127 of the
+    # row's absmax), so an fp32 reordering of ~1e-6 relative flips ~1e-3 of the
+    # values; each flip is held to one ulp above, the rate to < 1e-2
+    assert flips < 1e-2 * 24 * 2 * L * (3 * hid + inter), flips
+    dec.set_taps(0, 0)
+    lockstep(False)
     ref = _f16_reference_logits(w, seen[:6], oracle)
     dec.begin_synthetic(2, 0, 0, False)
     for s_, tok in enumerate(seen[:6]):
         dec.step(tok, logits_ptr=logits.data_ptr())
         torch.cuda.synchronize()
-        assert_parity(logits.cpu().numpy(), ref[s_], LOGIT_TOL, axis=1, what="vs float64")
+        assert rel_err(logits.cpu().numpy(), ref[s_]) < LOGIT_TOL
+    print(f"fp16 decoder H {H} S {S}: forced worst logit rel err {worst:.2e}, fp16 flips {flips}")
 
 
 def test_synthetic_long_context_step(gpu, oracle):
@@ -586,8 +630,9 @@ def test_prefill_decode_kernel_fallback(gpu, oracle):
         od = OracleDecoder(oracle, wf, 1)
         for i, t in enumerate(prompts[r]):
             _, ol, _ = od.step(np.array([t], np.int32), np.array([i], np.int32))
-        assert_parity(la[r], ol[0], LOGIT_TOL, what=f"row {r} stepping")
-        assert_parity(lb[r], ol[0], LOGIT_TOL, what=f"row {r} prefill")
+        # free running (prefill chunks are not tapped): tensor-normalised bound
+        assert rel_err(la[r], ol[0]) < LOGIT_TOL, (r, "stepping", rel_err(la[r], ol[0]))
+        assert rel_err(lb[r], ol[0]) < LOGIT_TOL, (r, "prefill", rel_err(lb[r], ol[0]))
         assert rel_err(lb[r], la[r]) < 2 * LOGIT_TOL, (r, rel_err(lb[r], la[r]))
         assert la[r].max() - la[r][nxt[r]] <= LOGIT_TOL * np.abs(la[r]).max()
     w = _int8_model(oracle, L=2, H=2, D=256, V=400, S=700, seed=13)

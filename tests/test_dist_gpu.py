@@ -56,14 +56,25 @@ def _tokens(mode, world, rank, global_rows):
 
 
 def _run(rows, world, rank, shard_rows, gather, first):
+    import torch
     import dist_decode
     dec = _decoder(rows)
-    sd = dist_decode.ShardedDecode(dist_decode.HipDecoderStep(dec), rows, V, world=world,
-                                   rank=rank, shard_rows=shard_rows, gather=gather,
-                                   staging="host", keep=True)
-    elapsed = dist_decode.timed_run(sd, WARMUP, STEPS, [int(t) for t in first],
-                                    timer_device="cpu")
-    return [t.numpy().copy() for t in sd.finish()], elapsed
+    with torch.cuda.stream(torch.cuda.Stream()):  # bench.py's explicit stream
+        sd = dist_decode.ShardedDecode(dist_decode.HipDecoderStep(dec), rows, V, world=world,
+                                       rank=rank, shard_rows=shard_rows, gather=gather,
+                                       staging="host", keep=True)
+        elapsed = dist_decode.timed_run(sd, WARMUP, STEPS, [int(t) for t in first],
+                                        timer_device="cpu")
+        return [t.numpy().copy() for t in sd.finish()], elapsed
+
+
+def test_hip_step_refuses_the_default_stream(gpu):
+    """torch's default stream is handle 0, which the C ABI reads as the
+    decoder's own (non-blocking) stream: HipDecoderStep refuses it rather than
+    letting staging copies and gathers race the step."""
+    import dist_decode
+    with pytest.raises(ValueError, match="non-default"):
+        dist_decode.HipDecoderStep(_decoder(1))
 
 
 def _worker(rank, world, port, mode, gather, global_rows, q):

@@ -6,7 +6,12 @@ paged attention of a prompt chunk, the reference's is_prefill pass
 Oracle: the CPU restatement run as a decode batch of m rows with
 beam_ids = row and context_lens = p0 + i + 1 — exactly the rows the decode
 kernel computed per prompt token before this kernel existed.  Tolerance as
-pa_decode: 1e-3 relative (max-abs error / max-abs reference)."""
+pa_decode: 1e-3 relative, tensor-normalised and elementwise.  The elementwise
+floor is ATOL_FRAC = 4e-6 of the largest |output| (decode: 1e-6): q and p
+enter the fp16 MFMAs as hi + lo halves, ~22 significant bits, so a score
+carries ~2.4e-7 x sum|q_i k_i| of error and an output element ~1e-6 of the
+output scale (measured 2e-7 .. 1.5e-6 of it, scripts/diag_prefill.py); an
+element near zero is held to that floor, every other to 1e-3 of itself."""
 import numpy as np
 import pytest
 
@@ -14,6 +19,7 @@ from _util import assert_parity, rel_err
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-3
+ATOL_FRAC = 4e-6
 
 
 def _dev(a):
@@ -75,12 +81,12 @@ def test_pa_prefill_vs_oracle(gpu, oracle, H, D, ts, p0, m, row, split):
                               split=split).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, row, p0)
     assert np.isfinite(out).all()
-    assert_parity(out, ref, RTOL)
+    assert_parity(out, ref, RTOL, ATOL_FRAC)
     # and the decode kernel on the same rows agrees
     dec = llm_capi.pa_decode(_dev(q), _dev(kp), _dev(vp), _dev(pt), T=p0 + m,
                              beam_ids=_dev(np.full(m, row, np.int32)),
                              context_lens=_dev(np.arange(p0 + 1, p0 + m + 1, dtype=np.int32)))
-    assert_parity(out, dec.cpu().numpy(), RTOL)
+    assert_parity(out, dec.cpu().numpy(), RTOL, ATOL_FRAC)
 
 
 def test_pa_prefill_missing_pages_and_scale(gpu, oracle):
@@ -93,7 +99,7 @@ def test_pa_prefill_missing_pages_and_scale(gpu, oracle):
     out = llm_capi.pa_prefill(_dev(q), _dev(kp), _dev(vp), _dev(pt), row=1, p0=p0,
                               sm_scale=0.5).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, 1, p0, sm_scale=0.5)
-    assert_parity(out, ref, RTOL)
+    assert_parity(out, ref, RTOL, ATOL_FRAC)
 
 
 def test_pa_prefill_all_missing_is_zero(gpu):
@@ -122,7 +128,7 @@ def test_pa_prefill_strided_q_interleaved_pools(gpu, oracle):
     wide[:, :H * D] = _dev(q.reshape(m, H * D))
     out = llm_capi.pa_prefill(wide, kv[:, 0], kv[:, 1], _dev(pt), row=0, p0=p0).cpu().numpy()
     ref = _oracle(oracle, q, kp, vp, pt, 0, p0)
-    assert_parity(out, ref, RTOL)
+    assert_parity(out, ref, RTOL, ATOL_FRAC)
 
 
 def test_pa_prefill_rejects_unsupported(gpu):
