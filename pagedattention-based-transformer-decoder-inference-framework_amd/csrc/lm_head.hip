@@ -37,12 +37,14 @@ namespace llm {
 // instead of 128, halving its share of the per-CU traffic (rocprof, C3 shape,
 // scripts/time_lm_head.py: 57.6 vs 73.3 us per launch, identical logits; M 16 /
 // 32 / 64 at K 768-2048: 16.2 vs 16.7, 45.2 vs 47.0, 24.2 vs 32.4 us)
-#ifndef LLM_LM_WAVES
-#define LLM_LM_WAVES 16
-#endif
-constexpr int kLmWaves = LLM_LM_WAVES;
+// Vocabulary tiles per workgroup (LmHeadArgs::tiles, <= 16: waves past it only
+// help stage x): the fewest that still give every CU at most ONE workgroup, so
+// no CU streams more than its share of E -- for V = 50257 (3142 tiles) 13 per
+// workgroup = 242 workgroups on 256 CUs, where 16 left 59 CUs idle (197
+// workgroups of 1 MiB of E each at C3).  At least 8, so small vocabularies do
+// not stage x once per tile.
+constexpr int kLmWaves = 16;
 constexpr int kLmThreads = 64 * kLmWaves;
-constexpr int kLmCols = 16 * kLmWaves;  // vocabulary rows per workgroup
 constexpr int kLmKChunk = 256;          // K per LDS stage (8 k-steps of 32)
 constexpr int kLmKs = kLmKChunk / 32;
 
@@ -53,6 +55,7 @@ struct LmHeadArgs {
   float* part_val;    // [M][nwg] max per (row, workgroup), or NULL
   int32_t* part_idx;  // [M][nwg]
   int M, V, K, nwg;
+  int tiles;  // vocabulary tiles (computing waves) per workgroup, <= kLmWaves
   int mode;  // 0; tuning build (LLM_LM_MODE): bit0 skip MFMA, bit1 skip x staging, bit2 skip E loads
 };
 
@@ -66,13 +69,15 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
   const int lane = lane_id();
   const int w = wave_id_uniform();
   const int m0 = blockIdx.y * 16 * MT;
-  const int n0 = blockIdx.x * kLmCols + w * 16;  // this wave's 16 vocabulary rows
+  const int ntile = blockIdx.x * a.tiles + w;  // this wave's 16 vocabulary rows
+  const int n0 = ntile * 16;
+  const bool mine = w < a.tiles;  // a wave past `tiles` only stages x
   const int KS = a.K / 32;
-  const int ntile = n0 >> 4;
   const int ntiles = (a.V + 15) / 16;
   const auto ers = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.E, (short)0, (uint32_t)min((size_t)ntiles * KS * 1024, (size_t)0xFFFFFFF0u), 0x00020000);
-  const uint32_t e_off = ntile < ntiles ? (uint32_t)((size_t)ntile * KS * 1024) + lane * 16 : 0xFFFFFFF0u;
+  const uint32_t e_off =
+      mine && ntile < ntiles ? (uint32_t)((size_t)ntile * KS * 1024) + lane * 16 : 0xFFFFFFF0u;
 
   f32x4 acc[MT];
 #pragma unroll
@@ -139,7 +144,9 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
       issue(nxt, c + 1);
       load_x(c + 1);
     }
-    if (a.mode & 1) {
+    if (!mine) {
+      // stages x only
+    } else if (a.mode & 1) {
       acc[0][0] += __builtin_bit_cast(float, cur[0][0] ^ cur[kLmKs - 1][3]) * 0.f +
                    (float)xa[0][0][0][lane][0];
     } else {
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
 
   // acc[mt] lane l, reg r: x row m0 + mt*16 + 4*(l>>4) + r, vocab row n0 + (l&15)
   // (C/D layout: col = lane&15 -> here the vocabulary index, row = 4*(lane>>4)+reg).
-  const int n = n0 + (lane & 15);
+  const int n = mine ? n0 + (lane & 15) : a.V;  // a staging-only wave stores nothing
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -195,7 +202,7 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
     if (m0 + row >= a.M) continue;
     float bv = pv[0][row];
     int bi = pi[0][row];
-    for (int ww = 1; ww < kLmWaves; ++ww)  // waves cover increasing vocabulary rows
+    for (int ww = 1; ww < a.tiles; ++ww)  // waves cover increasing vocabulary rows
       if (pv[ww][row] > bv) { bv = pv[ww][row]; bi = pi[ww][row]; }
     a.part_val[(size_t)(m0 + row) * a.nwg + blockIdx.x] = bv;
     a.part_idx[(size_t)(m0 + row) * a.nwg + blockIdx.x] = bi;
@@ -241,7 +248,36 @@ __global__ __launch_bounds__(256) void argmax_partials_kernel(const float* __res
   }
 }
 
-int lm_head_workgroups(int V) { return (V + kLmCols - 1) / kLmCols; }
+namespace {
+int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+  }
+  return cus;
+}
+}  // namespace
+
+int lm_head_tiles(int V) {
+#if LLM_TUNING
+  const int forced = env_int("LLM_LM_TILES", 0);  // tuning build: A/B of the tiles per workgroup
+  if (forced >= 1 && forced <= kLmWaves) return forced;
+#endif
+  const int ntiles = (V + 15) / 16;
+  const int cus = cu_count();
+  return std::min(kLmWaves, std::max(8, (ntiles + cus - 1) / cus));
+}
+
+int lm_head_workgroups(int V) {
+  const int t = lm_head_tiles(V);
+  return ((V + 15) / 16 + t - 1) / t;
+}
 
 // E [V][K] row-major -> B-fragment order: block (vocab tile t, k-step s) is
 // 1 KiB; lane l holds E[16 t + (l & 15)][32 s + 8 (l >> 4) + j], j < 8.
@@ -284,7 +320,7 @@ hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, i
   constexpr int mode = 0;
 #endif
   LmHeadArgs a{x, static_cast<const _Float16*>(E), logits, part_val, part_idx, M, V, K,
-               lm_head_workgroups(V), mode};
+               lm_head_workgroups(V), lm_head_tiles(V), mode};
   const int mt = M <= 16 ? 1 : M <= 32 ? 2 : 4;
   const dim3 grid(a.nwg, (M + 16 * mt - 1) / (16 * mt)), block(kLmThreads);
   if (mt == 1) hipLaunchKernelGGL(lm_head_kernel<1>, grid, block, 0, st, a);

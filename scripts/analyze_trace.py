@@ -22,8 +22,12 @@ t1 = max(r["e"] for r in step)
 print(f"step kernels {len(step)} span {(t1 - t0) / 1e3:.1f} us, queues {sorted({r['Queue_Id'] for r in step})}")
 kind = defaultdict(float)
 cnt = defaultdict(int)
+by_grid = "--by-grid" in sys.argv  # split each kernel kind by its grid (GEMM shapes)
 for r in step:
     k = re.sub(r"^void |llm::|\(.*$", "", r["Kernel_Name"])[:60]
+    if by_grid:
+        g = [r.get(c, "") for c in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z", "Grid_Size")]
+        k = f"{k} grid={'x'.join(x for x in g if x)} wg={r.get('Workgroup_Size_X', r.get('Workgroup_Size', ''))}"
     kind[k] += (r["e"] - r["s"]) / 1e3
     cnt[k] += 1
 for k, v in sorted(kind.items(), key=lambda kv: -kv[1]):

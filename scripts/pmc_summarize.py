@@ -41,9 +41,10 @@ def main():
                       "dispatches": f.get(k, {}).get("dispatches")}
     hbm = 0.0
     for k, v in kernels.items():
-        if "pa_split_kernel" in k or "pa_merge_kernel" in k:
+        if "pa_split_kernel" in k or "pa_merge_kernel" in k or "pa_merge_row_kernel" in k:
             hbm += 2.0 * (v["FETCH_SIZE_KiB"] or 0.0) * 1024 + (v["WRITE_SIZE_KiB"] or 0.0) * 1024
-    res = {"config": algo.get("config"), "pps": algo.get("pps"),
+    res = {"config": algo.get("config"), "pps": algo.get("pps"), "launch": algo.get("launch"),
+           "nsplit": algo.get("nsplit"), "form": algo.get("form"),
            "algorithmic_bytes_per_launch": algo["algorithmic_bytes"],
            "hbm_bytes_per_launch": int(hbm),
            "traffic_over_algorithmic": round(hbm / algo["algorithmic_bytes"], 4),

@@ -25,6 +25,7 @@ import llm_capi  # noqa: E402
 
 CFGS = {"c3": dict(B=64, H=16, D=128, T=8192, ts=16),
         "c2": dict(B=16, H=12, D=64, T=2048, ts=16),
+        "c5": dict(B=64, H=32, D=128, T=8192, ts=16),
         # C4: 8 sequences x 4 beams; each sequence's first 240 tiles are one
         # set of pages shared by its beams (kv_cache_fork), the last 16 private
         "c4": dict(B=32, H=16, D=128, T=4096, ts=16, beams=4, shared=240)}
@@ -32,9 +33,52 @@ CFGS = {"c3": dict(B=64, H=16, D=128, T=8192, ts=16),
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c3", choices=sorted(CFGS))
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--decoder", action="store_true",
+                help="time the decoder's own attention launch (llm_decoder_run_attention: the "
+                     "step graph's kernels and outputs) of a 1-layer decoder of the config's dims")
 args = ap.parse_args()
 c = CFGS[args.config]
 B, H, D, T, ts = c["B"], c["H"], c["D"], c["T"], c["ts"]
+W = c.get("beams", 1)
+if args.decoder:
+    sys.path.insert(0, str(ROOT))
+    import numpy as np  # noqa: E402
+    import llm_decoder  # noqa: E402
+    from bench import make_weights  # noqa: E402
+    cls = "CUDADecoder" if args.config == "c2" else "INT8Decoder"
+    cfg = dict(cls=cls, L=1, H=H, D=D, V=512)
+    dec = getattr(llm_decoder, cls)(1, H, D, H * D, 512, T + 8, max_batch=B, page_size=ts)
+    dec.set_weights(make_weights(cfg, 5))
+    if W > 1:
+        dec.begin_beams(B // W, W, c["shared"] * ts, T - c["shared"] * ts, 3, True)
+    else:
+        dec.begin_synthetic(B, T, 3, True)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    st = torch.cuda.current_stream().cuda_stream
+    dec.step(list(range(B)), stream=st)  # q rows of a real step; context T + 1
+    T = dec.context_len(0)
+    nt = (T + ts - 1) // ts
+    nsplit, form = dec.attention_plan()
+
+    def launch():
+        dec.run_attention(0, st)
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(args.iters):
+        launch()
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / args.iters * 1e-3
+    kv_tiles = B * H * nt if W == 1 else (B // W) * H * (c["shared"] + W * (nt - c["shared"]))
+    nbytes = 2 * kv_tiles * ts * D * 2 + B * H * nt * 4 + 2 * B * H * D * 4
+    print(json.dumps({"config": args.config, "launch": "decoder (llm_decoder_run_attention)",
+                      "nsplit": nsplit, "form": form, "T": T, "iters": args.iters,
+                      "us_per_launch": round(t * 1e6, 2), "algorithmic_bytes": nbytes,
+                      "GBps": round(nbytes / t / 1e9, 1)}))
+    sys.exit(0)
 nt = (T + ts - 1) // ts
 num_pages = B * H * nt
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -44,7 +88,6 @@ kv[:, 0] *= D ** -0.25
 kp, vp = kv[:, 0], kv[:, 1]
 q = torch.randn((B, H, D), generator=g, device="cuda") * D ** -0.25
 pt = torch.randperm(num_pages, generator=g, device="cuda").to(torch.int32).reshape(B, H, nt)
-W = c.get("beams", 1)
 if W > 1:  # beams of a sequence alias the first `shared` page ids of its first beam
     sh = c["shared"]
     pt = pt.reshape(B // W, W, H, nt).clone()
