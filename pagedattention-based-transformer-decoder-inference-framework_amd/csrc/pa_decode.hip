@@ -76,6 +76,7 @@ struct PaSplitArgs {
   _Float16* out16;
   int pack;
   int wgm;
+  int beam4;  // row_group 4: pa_beam4_kernel (one wave per (group, head, split))
 };
 
 constexpr int kWgmMaxSplits = 8;  // one merge batch (pa_merge_row_kernel's kMergeBatch)
@@ -590,6 +591,274 @@ void pa_split_kernel(PaSplitArgs a) {
     }
   }
 }
+
+#if LLM_TUNING
+// Beam-group attention, one WAVE per (group of 4 beams, head, split): the
+// wave loads each KV page ONCE into registers and runs the math of every beam
+// that reads it (row_group 4, fp16 pools, pages <= 8 KiB).  A split's work is
+// a list of page items: a page all 4 beams share (the group's leading tiles
+// whose page ids agree in all 4 rows -- a forked prefix) is one item for all 4
+// beams; a beam-private page is one item for its beam.  The items of a
+// (group, head) are cut into nsplit equal runs (equal HBM bytes per wave:
+// every item is one page), so no LDS, no barrier and no per-beam re-load;
+// each beam keeps its own online-softmax state and the wave writes one split
+// partial per beam, merged by pa_merge_row_kernel (every split holds one).
+// Groups whose rows differ in context, route outside the table or do not all
+// exist take the same kernel beam by beam (items of one beam, its own context,
+// its own equal split of its tiles).
+// Maths per beam as pa_split_kernel (log2 units, row groups of the wave merged
+// at the end), so results match the plain schedule up to the split boundaries.
+// MINW: waves per SIMD asked of the register allocator; U: page items per
+// register stage (two stages in flight).
+template <int D, int TS, int MINW = 2, int U = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void pa_beam4_kernel(PaSplitArgs a) {
+  constexpr int G = 4;
+  constexpr int EPL = 8;  // fp16 elements per 16-byte lane load
+  constexpr int LPT = D / EPL;
+  constexpr int TPI = 64 / LPT;
+  constexpr int NI = TS / TPI;
+  constexpr int PAGE_BYTES = TS * D * 2;
+  static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1 && PAGE_BYTES <= 8192,
+                "pa_beam4_kernel: fp16 pages of 1..8 KiB");
+  const int lane = lane_id();
+  const int wid = blockIdx.x * 4 + wave_id_uniform();
+  const int s = wid % a.nsplit;
+  const int gh = wid / a.nsplit;
+  const int h = gh % a.H;
+  const int grp = gh / a.H;
+  if (grp >= (a.B + G - 1) / G) return;
+  const int b0 = grp * G;
+  const int c = lane % LPT;
+  const int g = lane / LPT;
+
+  // the group's rows (wave-uniform): page-table row, context, existence
+  int prow_off[G], Tg[G];
+  bool live[G];
+  bool share = true;
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    const int bi = b0 + i;
+    live[i] = bi < a.B;
+    int ri = -1, Ti = 0;
+    if (live[i]) {
+      ri = a.beam_ids ? a.beam_ids[bi] : bi;
+      Ti = a.context_lens ? a.context_lens[bi] : a.T;
+      Ti = min(max(Ti, 0), a.T);
+    }
+    const bool rok = ri >= 0 && ri < a.num_beams;
+    prow_off[i] = rok ? (ri * a.H + h) * a.max_tiles : -1;
+    Tg[i] = rok ? Ti : 0;  // a row outside the table reads nothing (all pages missing)
+    if (!live[i] || !rok || Ti != Tg[0]) share = false;
+  }
+
+  // q of each beam (dims c*8 .. c*8+7), pre-scaled into log2 units
+  float qv[G][EPL];
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    const float* qp = a.q + (size_t)min(b0 + i, a.B - 1) * a.q_stride + (size_t)h * D + c * EPL;
+    const f32x4 q0 = *reinterpret_cast<const f32x4*>(qp);
+    const f32x4 q1 = *reinterpret_cast<const f32x4*>(qp + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      qv[i][e] = q0[e] * a.qscale;
+      qv[i][4 + e] = q1[e] * a.qscale;
+    }
+  }
+  float m[G], l[G], acc[G][EPL];
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    m[i] = kNegSentinel;
+    l[i] = 0.f;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) acc[i][e] = 0.f;
+  }
+  const uint32_t lane_off = (uint32_t)lane * 16u;
+
+  // One segment = a list of <= 128 page items, lane j holding item j and 64 + j
+  // (page id, and tile << 4 | beam mask); shared groups have one segment,
+  // the others one per beam.
+  const int nseg = share ? 1 : G;
+  for (int seg = 0; seg < nseg; ++seg) {
+    int i0 = 0, cnt = 0, nsh = 0, ntiles = 0;
+    if (share) {
+      ntiles = min((Tg[0] + TS - 1) / TS, a.max_tiles);
+      for (int blk = 0; blk < ntiles; blk += 64) {  // the shared prefix, 64 tiles per round
+        const int t = blk + lane;
+        bool eq = t < ntiles;
+        if (eq) {
+          const int32_t p0 = a.page_table[prow_off[0] + t];
+#pragma unroll
+          for (int i = 1; i < G; ++i) eq = eq && a.page_table[prow_off[i] + t] == p0;
+        }
+        const uint64_t mk = __ballot(eq);
+        const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
+        nsh = blk + run;
+        if (run < 64) break;
+      }
+      nsh = min(nsh, ntiles);
+      const int items = nsh + G * (ntiles - nsh);
+      i0 = (int)(((long long)items * s) / a.nsplit);
+      cnt = (int)(((long long)items * (s + 1)) / a.nsplit) - i0;
+    } else {
+      if (prow_off[seg] < 0) continue;  // no such row / outside the table: a neutral partial
+      ntiles = min((Tg[seg] + TS - 1) / TS, a.max_tiles);
+      const int pps = row_pps(0, a.nsplit, ntiles);
+      i0 = s * pps;
+      cnt = min(pps, ntiles - i0);
+    }
+    cnt = min(cnt, kMaxPps);  // the host sizes nsplit so a split holds <= 128 items
+    if (cnt <= 0) continue;
+    const int npriv = ntiles - nsh;
+    int pid[2], inf[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int j = lane + 64 * r;
+      pid[r] = -1;
+      inf[r] = 0;
+      if (j < cnt) {
+        const int k = i0 + j;
+        int tile, beam, mask;
+        if (!share) {
+          tile = k; beam = seg; mask = 1 << seg;
+        } else if (k < nsh) {
+          tile = k; beam = 0; mask = 0xF;
+        } else {  // beam-major: a beam's private tiles are consecutive items
+          const int p = k - nsh;
+          beam = p / npriv; tile = nsh + p % npriv; mask = 1 << beam;
+        }
+        int id = a.page_table[prow_off[beam] + tile];
+        pid[r] = id >= a.num_pages ? -1 : id;
+        inf[r] = (tile << 4) | mask;
+      }
+    }
+    auto item_pid = [&](int j) {
+      return j < 64 ? __builtin_amdgcn_readlane(pid[0], j) : __builtin_amdgcn_readlane(pid[1], j - 64);
+    };
+    auto item_inf = [&](int j) {
+      return j < 64 ? __builtin_amdgcn_readlane(inf[0], j) : __builtin_amdgcn_readlane(inf[1], j - 64);
+    };
+    auto issue = [&](u32x4 (&kk)[NI], u32x4 (&vv)[NI], int j) {
+      const int pg = j < cnt ? item_pid(min(j, kMaxPps - 1)) : -1;
+      const bool ok = pg >= 0;
+      const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
+      const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k_pool + off), (short)0,
+                                                         ok ? PAGE_BYTES : 0, 0x00020000);
+      const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.v_pool + off), (short)0,
+                                                         ok ? PAGE_BYTES : 0, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        kk[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_off + i * 1024, 0, kKvLoadAux);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        vv[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_off + i * 1024, 0, kKvLoadAux);
+    };
+    // one page item for beam bi: scores, online softmax, p.v (pa_split_kernel maths)
+    auto beam_math = [&](auto full_tag, auto beam_tag, const u32x4 (&kk)[NI],
+                         const u32x4 (&vv)[NI], bool ok, int tok_base, int Tb) {
+      constexpr bool FULL = decltype(full_tag)::value;
+      constexpr int bi = decltype(beam_tag)::value;
+      float sc[NI];
+      bool valid[NI];
+      float mloc = kNegSentinel;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) d = fmaf(qv[bi][e], kv_at<LLM_F16>(kk[i], e), d);
+        d = group_sum<LPT>(d);
+        valid[i] = FULL || (ok && (tok_base + i * TPI) < Tb);
+        sc[i] = valid[i] ? d : kNegSentinel;
+        mloc = fmaxf(mloc, sc[i]);
+      }
+      const float mnew = fmaxf(m[bi], mloc);
+      const float corr = __builtin_amdgcn_exp2f(m[bi] - mnew);
+      l[bi] *= corr;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[bi][e] *= corr;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const float p = valid[i] ? __builtin_amdgcn_exp2f(sc[i] - mnew) : 0.f;
+        l[bi] += p;
+        const u32x4 vraw = FULL || valid[i] ? vv[i] : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) acc[bi][e] = fmaf(p, kv_at<LLM_F16>(vraw, e), acc[bi][e]);
+      }
+      m[bi] = mnew;
+    };
+    auto compute = [&](const u32x4 (&kk)[NI], const u32x4 (&vv)[NI], int j) {
+      const int pg = item_pid(min(j, kMaxPps - 1));
+      const int info = item_inf(min(j, kMaxPps - 1));
+      const int tile = info >> 4, mask = info & 0xF;
+      const bool ok = pg >= 0;
+      const int Tb = share ? Tg[0] : Tg[seg];
+      const bool full = ok && (tile + 1) * TS <= Tb;
+      const int tok_base = tile * TS + g;
+      auto each = [&](auto beam_tag) {
+        constexpr int bi = decltype(beam_tag)::value;
+        if (mask & (1 << bi)) {
+          if (full)
+            beam_math(std::true_type{}, beam_tag, kk, vv, ok, tok_base, Tb);
+          else
+            beam_math(std::false_type{}, beam_tag, kk, vv, ok, tok_base, Tb);
+        }
+      };
+      each(std::integral_constant<int, 0>{});
+      each(std::integral_constant<int, 1>{});
+      each(std::integral_constant<int, 2>{});
+      each(std::integral_constant<int, 3>{});
+    };
+    u32x4 kA[U][NI], vA[U][NI], kB[U][NI], vB[U][NI];
+    auto issue_st = [&](u32x4 (&kk)[U][NI], u32x4 (&vv)[U][NI], int j0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) issue(kk[u], vv[u], j0 + u);  // past the end: no bytes
+    };
+    auto compute_st = [&](const u32x4 (&kk)[U][NI], const u32x4 (&vv)[U][NI], int j0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j0 + u < cnt) compute(kk[u], vv[u], j0 + u);
+    };
+    issue_st(kA, vA, 0);
+    for (int j = 0; j < cnt; j += 2 * U) {
+      issue_st(kB, vB, j + U);
+      compute_st(kA, vA, j);
+      if (j + U >= cnt) break;
+      issue_st(kA, vA, j + 2 * U);
+      compute_st(kB, vB, j + U);
+    }
+  }
+
+  // Per beam: merge the TPI row groups of the wave, write the split partial.
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+#pragma unroll
+    for (int off = LPT; off < 64; off <<= 1) {
+      const float mo = __shfl_xor(m[i], off, 64);
+      const float lo = __shfl_xor(l[i], off, 64);
+      const float mn = fmaxf(m[i], mo);
+      const float ca = __builtin_amdgcn_exp2f(m[i] - mn);
+      const float cb = __builtin_amdgcn_exp2f(mo - mn);
+      l[i] = l[i] * ca + lo * cb;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const float ao = __shfl_xor(acc[i][e], off, 64);
+        acc[i][e] = acc[i][e] * ca + ao * cb;
+      }
+      m[i] = mn;
+    }
+    if (!live[i]) continue;
+    const size_t pidx = ((size_t)(b0 + i) * a.H + h) * a.nsplit + s;
+    if (lane < LPT) {
+      float* o = a.part_acc + pidx * D + c * EPL;
+      *reinterpret_cast<f32x4*>(o) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{acc[i][4], acc[i][5], acc[i][6], acc[i][7]};
+    }
+    if (lane == 0) {
+      a.part_ml[pidx * 2] = m[i];
+      a.part_ml[pidx * 2 + 1] = l[i];
+    }
+  }
+}
+#endif  // LLM_TUNING
 
 #if LLM_TUNING
 // Tuning build only (LLM_BEAM_MFMA=1): measured slower than the VALU BEAM form
@@ -1240,6 +1509,64 @@ long long resident_waves() {
 // The MFMA beam-group kernel (D 128, page 16) exists only in the tuning build
 // (LLM_BEAM_MFMA=1).  A private page costs it 4 items to a shared page's 1:
 // split balance 64/16.
+// The one-wave-per-beam-group kernel (pa_beam4_kernel) for row_group 4 fp16
+// launches, tuning build only (LLM_BEAM4=1; LLM_BEAM4_SPLITS forces its split
+// count): measured slower than the LDS-staged BEAM form of pa_split_kernel
+// (C4 launch with merge: 69.2 us at 16 splits, 74.2 with two pages per
+// register stage, 82.3 at 12 splits, against 67.6 us).
+#ifndef BEAM4_MINW
+#define BEAM4_MINW 2
+#endif
+#ifndef BEAM4_U
+#define BEAM4_U 1
+#endif
+bool beam4_on() {
+#if LLM_TUNING
+  return env_int("LLM_BEAM4", 0) != 0;  // read per launch
+#else
+  return false;
+#endif
+}
+
+#if LLM_TUNING
+template <int D, int TS>
+long long beam4_resident_waves() {
+  if constexpr (TS * D * 2 > 8192) {
+    return 0;
+  } else {
+  static long long cached = 0;
+  if (cached) return cached;
+  int dev = 0, cus = 0, blocks = 0;
+  if (hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, pa_beam4_kernel<D, TS, BEAM4_MINW, BEAM4_U>, 256, 0) ==
+          hipSuccess &&
+      cus > 0 && blocks > 0) {
+    cached = (long long)cus * blocks * 4;
+  } else {
+    (void)hipGetLastError();
+    cached = 256LL * 4 * 3;
+  }
+  return cached;
+  }
+}
+
+long long beam4_resident_for(int D, int TS) {
+  auto by_ts = [&](auto d) -> long long {
+    constexpr int DD = decltype(d)::value;
+    return TS == 16 ? beam4_resident_waves<DD, 16>() : beam4_resident_waves<DD, 32>();
+  };
+  switch (D) {
+    case 32: return by_ts(std::integral_constant<int, 32>{});
+    case 64: return by_ts(std::integral_constant<int, 64>{});
+    case 128: return by_ts(std::integral_constant<int, 128>{});
+    default: return by_ts(std::integral_constant<int, 256>{});
+  }
+}
+#else
+long long beam4_resident_for(int, int) { return 0; }
+#endif
+
 bool beam_mfma_on() {
 #if LLM_TUNING
   return env_int("LLM_BEAM_MFMA", 0) != 0;  // read per launch: a test sets and restores it
@@ -1287,6 +1614,17 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
                        dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
     return hipGetLastError();
   }
+#if LLM_TUNING
+  if (a.group == 4 && !direct && ST == 2 && a.beam4) {
+    // pa_beam4_kernel: one wave per (group, head, split)
+    const int waves4 = ((a.B + 3) / 4) * a.H * a.nsplit;
+    if constexpr (TS * D * 2 <= 8192)
+      hipLaunchKernelGGL((pa_beam4_kernel<D, TS, BEAM4_MINW, BEAM4_U>), dim3((waves4 + 3) / 4), dim3(256), 0,
+                         st, a);
+    *beam = true;
+    return hipGetLastError();
+  }
+#endif
   if (a.group == 4 && !direct && ST == 2) {
     // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
     // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
@@ -1626,6 +1964,27 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     if (f >= 2 && f <= kWgmMaxSplits && (long long)f * kMaxPps >= ntiles_max) nsplit = f;
   }
 #endif
+  // beam groups of 4 rows (fp16 pages <= 8 KiB, dynamic splits): pa_beam4_kernel,
+  // one wave per (group, head, split), splits sized for its own occupancy (a
+  // whole number of resident rounds over (group, head) pairs), each split
+  // holding <= 128 page items; fixed pages_per_split keeps the BEAM form
+  bool use_beam4 = false;
+  if (row_group == 4 && pps_fixed <= 0 && kv->kv_dtype == LLM_F16 && TS * D * 2 <= 8192 &&
+      beam4_on() && !beam_mfma_on()) {
+    const long long groups = (long long)((B + 3) / 4) * H;
+    const long long need = (4LL * ntiles_max + kMaxPps - 1) / kMaxPps;
+    long long ns = (beam4_resident_for(D, TS) + groups - 1) / groups;
+    ns = std::max(std::max(ns, need), 2LL);
+    ns = std::min(ns, max_nsplit(B, H, ntiles_max));
+#if LLM_TUNING
+    const int f = env_int("LLM_BEAM4_SPLITS", 0);
+    if (f >= 2) ns = std::min<long long>(f, max_nsplit(B, H, ntiles_max));
+#endif
+    if (ns >= need && ns >= 2) {
+      use_beam4 = true;
+      nsplit = (int)ns;
+    }
+  }
   if (nsplit > kMaxSplits || (long long)nsplit * (pps_fixed > 0 ? pps_fixed : kMaxPps) < ntiles_max)
     return fail(LLM_ERR_UNSUPPORTED,
                 "pa_decode: at most 128 splits of at most 128 pages per row (raise "
@@ -1672,6 +2031,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   }
   a.balance16 = beam_balance16();
+  a.beam4 = use_beam4 ? 1 : 0;
   const bool wgm = wgm_ok && !direct && a.group == 1 && nsplit <= kWgmMaxSplits;
   if (wgm) {
     a.wgm = 1;

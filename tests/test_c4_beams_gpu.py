@@ -95,7 +95,8 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     empty splits, ragged contexts, beam_ids routing inside a group, a missing
     shared page, and never-written (NaN) token rows past every context in both
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
-    cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1)."""
+    cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1)
+    and its one-wave-per-group kernel (LLM_BEAM4=1)."""
     import torch
     import llm_capi
     rng = np.random.default_rng(B * 7 + T)
@@ -160,3 +161,12 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     assert np.isfinite(outm).all()
     assert_parity(outm, ref, 1e-3)
     assert rel_err(outm, plain) < 1e-5
+    # ... and its one-wave-per-beam-group kernel (pa_beam4_kernel, LLM_BEAM4=1)
+    monkeypatch.setenv("LLM_BEAM_MFMA", "0")
+    monkeypatch.setenv("LLM_BEAM4", "1")
+    out4 = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                              beam_ids=d(beam_ids), row_group=4,
+                              lib=llm_capi.load_tune()).cpu().numpy()
+    assert np.isfinite(out4).all()
+    assert_parity(out4, ref, 1e-3)
+    assert rel_err(out4, plain) < 1e-5
