@@ -75,6 +75,7 @@ struct llm_decoder {
   DevBuf<uint8_t> wqkv, wo, w1, w2;  // packed, L consecutive blocks
   size_t sz_qkv = 0, sz_o = 0, sz_1 = 0, sz_2 = 0;
   bool weights_ready = false;
+  int w_keep = 0;  // the GEMM weights fit the Infinity Cache: keep them there (w_keep_for)
 
   // KV
   kv_cache* kv = nullptr;
@@ -272,6 +273,18 @@ static int upload_common(llm_decoder* d, const uint16_t* emb, const float* ln1_g
   return LLM_OK;
 }
 
+// The weight GEMMs load with the default cache policy (lines stay in the
+// 256 MiB Infinity Cache, so the next step's GEMMs hit there) when the whole
+// weight set fits well inside it; the KV stream is loaded non-temporal and
+// does not displace them.  Larger models stream their weights nt (read once
+// per step: keeping them would only churn the cache).  Same-box A/B, two
+// runs each (profiles/r03/wkeep_ab.txt): C2 (170 MB of weights) +1.7 / +2.1 %
+// kept; C4 (1.2 GB) -2.3 / -2.6 % kept, so nt there.
+static int w_keep_for(const llm_decoder* d) {
+  const size_t bytes = (d->sz_qkv + d->sz_o + d->sz_1 + d->sz_2) * (size_t)d->L;
+  return bytes <= (size_t)192 << 20;
+}
+
 extern "C" int llm_decoder_set_int8_weights(llm_decoder* d, const llm_int8_weights* w) {
   LLM_REQUIRE(d && w, "llm_decoder_set_int8_weights: NULL");
   LLM_REQUIRE(d->wdtype == LLM_I8, "llm_decoder_set_int8_weights: decoder is not INT8");
@@ -289,6 +302,8 @@ extern "C" int llm_decoder_set_int8_weights(llm_decoder* d, const llm_int8_weigh
   RET_IF(upload(d->sw2, w->sw2, (size_t)L * hid, "sw2"));
   RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
   RET_IF(upload(d->b2, w->b2, (size_t)L * hid, "b2"));
+  d->w_keep = w_keep_for(d);
+  d->graph_batch = -1;
   d->weights_ready = true;
   return LLM_OK;
 }
@@ -306,6 +321,8 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
   RET_IF(upload_packed(d->w2, d->sz_2, w->w2, L, inter, hid, LLM_F16, "w2"));
   RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
   RET_IF(upload(d->b2, w->b2, (size_t)L * hid, "b2"));
+  d->w_keep = w_keep_for(d);
+  d->graph_batch = -1;
   d->weights_ready = true;
   return LLM_OK;
 }
@@ -364,6 +381,7 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   WeightGemm g;
   g.dtype = wdtype;
   g.a_packed = 1;
+  g.w_keep = w_keep;
   g.A = R.act;
   g.W_packed = wqkv.p + sz_qkv * l;
   g.M = R.n; g.N = 3 * hid; g.K = hid;
@@ -451,6 +469,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   WeightGemm g;
   g.dtype = wdtype;
   g.a_packed = 1;
+  g.w_keep = w_keep;
   g.A = R.act;
   g.M = R.n;
   // o_proj: input produced (packed) by the attention merge

@@ -69,12 +69,21 @@ struct GemmArgs {
   const float* ln_g;      // [K]
   const float* ln_b;      // [K]
   float ln_eps;
-  uint8_t* act_out;       // optional: workgroups with blockIdx.x == 0 store A (packed-A order)
+  uint8_t* act_out;       // optional: workgroups of column block 0 store A (packed-A order)
   float* sa_out;          //   and the I8 row scales (activation taps)
   // split-K (I8, gridDim.z = k slices): slice z sums k-steps [z KS/Z, (z+1) KS/Z)
   // and stores its exact int32 partial sums to acc_out + z * M * N ([M][N]),
   // nothing else; the consumer adds the slices and applies the epilogue.
   int partial;
+  // 1: weights loaded with the default cache policy (a model whose weights fit
+  // the 256 MiB Infinity Cache keeps them there from step to step); 0: nt
+  // (streamed once per step, not kept: larger models)
+  int w_keep;
+  // split-K only: 1 = workgroups remapped so that slice z runs on XCDs
+  // [z 8/Z, (z+1) 8/Z) (dispatch places linear workgroup i on XCD i % 8), so
+  // each XCD's L2 fetches only its slices' A columns instead of all of A
+  // (launch_gemm checks 8 % Z == 0 and tiles * Z % 8 == 0)
+  int xcd_map;
 };
 
 // LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
@@ -95,11 +104,12 @@ __device__ __forceinline__ unsigned long long phase_clock() {
 
 // k-steps per pipeline batch (two batches in flight): bounded by the VGPRs of
 // the A fragments (MT tiles, x2 for the fp32 LM-head A) held per k-step.
-template <int MT, int WAVES>
+template <int MT, int WAVES, int NT = 1>
 constexpr int gemm_unroll() {
   // 4-wave workgroups carry twice the k-steps per wave: twice the batch, so
-  // the same bytes are in flight from half the waves
-  return (MT >= 4 ? 2 : 4) * (WAVES == 4 ? 2 : 1);
+  // the same bytes are in flight from half the waves; 4 column tiles hold
+  // twice the fragments per k-step, so half the k-steps
+  return (MT >= 4 ? 2 : 4) * (WAVES == 4 ? 2 : 1) / (NT >= 4 ? 2 : 1);
 }
 
 __device__ __forceinline__ float apply_act(float y, int act) {
@@ -197,7 +207,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   using Tr = GemmTraits<KIND>;
   using acc_t = typename Tr::acc_t;
   constexpr int KSTEP = Tr::KSTEP;
-  constexpr int kUnroll = gemm_unroll<MT, WAVES>();
+  constexpr int kUnroll = gemm_unroll<MT, WAVES, NT>();
   // Cross-wave partial sums, [wave][tile][reg][lane]: lane-fastest so both the
   // per-register stores and the epilogue's reads (consecutive threads =
   // consecutive columns = consecutive lanes) are bank-conflict free.  With the
@@ -220,17 +230,27 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
 
   const int lane = lane_id();
   const int w = wave_id_uniform();
-  const int nt0 = blockIdx.x * NT;
-  const int m0 = blockIdx.y * 16 * MT;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (a.xcd_map) {
+    const int per = 8 / (int)gridDim.z;  // XCDs per k slice
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = lin & 7;
+    const int tile = (lin >> 3) * per + xcd % per;
+    bz = xcd / per;
+    bx = tile % (int)gridDim.x;
+    by = tile / (int)gridDim.x;
+  }
+  const int nt0 = bx * NT;
+  const int m0 = by * 16 * MT;
   unsigned long long* stamp =
-      a.stamps ? a.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 48 : nullptr;
+      a.stamps ? a.stamps + ((size_t)by * gridDim.x + bx) * 48 : nullptr;
   if (stamp && lane == 0) stamp[w] = phase_clock();  // [0, 16): wave start
-  // Wave w streams k range wr = (w + blockIdx.x) % WAVES: at any moment the
+  // Wave w streams k range wr = (w + bx) % WAVES: at any moment the
   // workgroups of an XCD read different A fragments (all of them read all of
   // A), instead of every workgroup hitting the same L2 lines.
-  const int wr = (w + blockIdx.x) % WAVES;
-  const int kz0 = (int)((blockIdx.z * a.KS) / gridDim.z);  // this k slice (split-K)
-  const int kzn = (int)(((blockIdx.z + 1) * a.KS) / gridDim.z) - kz0;
+  const int wr = (w + bx) % WAVES;
+  const int kz0 = (int)((bz * a.KS) / (int)gridDim.z);  // this k slice (split-K)
+  const int kzn = (int)(((bz + 1) * a.KS) / (int)gridDim.z) - kz0;
   const int ks0 = kz0 + (wr * kzn) / WAVES;
   const int ks1 = kz0 + ((wr + 1) * kzn) / WAVES;
   const int ntiles = (a.N + 15) >> 4;
@@ -284,7 +304,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       for (int j = 0; j < NT; ++j) {
         if (!do_b) break;
         const uint32_t boff = ok ? b_lane_off[j] + (uint32_t)kk * 1024u : 0xFFFFFFF0u;
-        bt.b[u][j] = __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff, 0, 2);
+        bt.b[u][j] = a.w_keep ? __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff, 0, 0)
+                              : __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff, 0, 2);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
@@ -373,7 +394,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
         if (o < ROWS * COLS) e_scale[e] *= sa_lds[o / COLS];
       }
     }
-    if (a.act_out && blockIdx.x == 0) {  // activation taps: A in packed-A order + scales
+    if (a.act_out && bx == 0) {  // activation taps: A in packed-A order + scales
       const int KS = a.KS;
       for (int i = threadIdx.x; i < ROWS_ * KS * 4; i += NTHR) {
         const int r = i / (KS * 4), g = i % (KS * 4);
@@ -426,7 +447,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int j = 0; j < NT; ++j) x ^= (int32_t)acc[mt][j][0] ^ (int32_t)acc[mt][j][3];
-    if (lane == 0 && a.C) a.C[blockIdx.x] = (float)x;
+    if (lane == 0 && a.C) a.C[bx] = (float)x;
     if (stamp && lane == 0) stamp[32 + w] = phase_clock();
     return;
   }
@@ -461,7 +482,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][reg][src_lane];
       if (a.partial) {
-        a.acc_out[((size_t)blockIdx.z * a.M + m) * a.N + n] = s;
+        a.acc_out[((size_t)bz * a.M + m) * a.N + n] = s;
         continue;
       }
       if (a.acc_out) a.acc_out[(size_t)m * a.N + n] = s;
@@ -535,21 +556,28 @@ template <GemmKind KIND, int MT, int NT>
 hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t st, int kslices) {
   const int ntiles = (a.N + 15) / 16;
   const dim3 grid((ntiles + NT - 1) / NT, mblocks, kslices);
-  if (a.ln_x) {
-    const size_t lds = ln_lds_bytes<KIND, MT, NT, 8>(a.K);
-    hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1>), grid, dim3(512), lds, st, a);
-    return hipGetLastError();
+  if constexpr (NT <= 2) {
+    if (a.ln_x) {
+      const size_t lds = ln_lds_bytes<KIND, MT, NT, 8>(a.K);
+      hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1>), grid, dim3(512), lds, st, a);
+      return hipGetLastError();
+    }
   }
-  if (waves == 4)
-    hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 4>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8>), grid, dim3(512), 0, st, a);
+  // the cross-wave sums' static LDS (WAVES x MT NT KiB) must stay <= 64 KiB
+  if constexpr (MT * NT * 8 <= 64) {
+    if (waves != 4) {
+      hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8>), grid, dim3(512), 0, st, a);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 4>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 template <GemmKind KIND, int MT>
 hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hipStream_t st,
                           int kslices) {
+  if (NT == 4 && !a.ln_x) return launch_gemm_nt<KIND, MT, 4>(a, waves, mblocks, st, kslices);
   return NT == 2 ? launch_gemm_nt<KIND, MT, 2>(a, waves, mblocks, st, kslices)
                  : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st, kslices);
 }
@@ -598,8 +626,9 @@ inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
 }
 
 template <GemmKind KIND>
-hipError_t launch_gemm(const GemmArgs& a, hipStream_t st, int nt_override = 0,
-                       int waves_override = 0, int mrows_override = 0) {
+hipError_t launch_gemm(const GemmArgs& a_in, hipStream_t st, int nt_override = 0,
+                       int waves_override = 0, int mrows_override = 0, int ks_override = 0) {
+  GemmArgs a = a_in;
   TileChoice tc{0, 0, 0};
   const bool narrow = nt_override == 0 && waves_override == 0 && mrows_override == 0 &&
                       narrow_decode_tile(a, GemmTraits<KIND>::KSTEP, tc);
@@ -619,10 +648,13 @@ hipError_t launch_gemm(const GemmArgs& a, hipStream_t st, int nt_override = 0,
   // Infinity Cache); split-K fills them with k slices instead
   if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256 && !a.ln_x && !a.partial) mrows = 32;
   if (mrows_override > 0) mrows = mrows_override;
-  const int ks = a.partial ? gemm_kslices(a.N, a.M, a.KS) : 1;
-  if (mrows == 16) return launch_gemm_mt<KIND, 1>(a, NT, waves, (a.M + 15) / 16, st, ks);
-  if (mrows == 32) return launch_gemm_mt<KIND, 2>(a, NT, waves, (a.M + 31) / 32, st, ks);
-  return launch_gemm_mt<KIND, 4>(a, NT, waves, (a.M + 63) / 64, st, ks);
+  const int ks = !a.partial ? 1 : ks_override > 0 ? ks_override : gemm_kslices(a.N, a.M, a.KS);
+  const int mblocks = (a.M + mrows - 1) / mrows;
+  const int tiles = ((a.N + 15) / 16 + NT - 1) / NT * mblocks;
+  if (a.xcd_map && (ks < 2 || 8 % ks != 0 || (tiles * ks) % 8 != 0)) a.xcd_map = 0;
+  if (mrows == 16) return launch_gemm_mt<KIND, 1>(a, NT, waves, mblocks, st, ks);
+  if (mrows == 32) return launch_gemm_mt<KIND, 2>(a, NT, waves, mblocks, st, ks);
+  return launch_gemm_mt<KIND, 4>(a, NT, waves, mblocks, st, ks);
 }
 
 }  // namespace
@@ -743,6 +775,7 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.ln_emb = g.ln_emb; a.ln_tok = g.ln_tok; a.ln_V = g.ln_V;
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;
+  a.w_keep = g.w_keep;
   if (g.partial) {
     LLM_REQUIRE(g.dtype == LLM_I8 && g.acc_out && !g.ln_x && !g.kv && !g.C16,
                 "weight_gemm: split-K is an I8 GEMM writing only int32 partials");
@@ -827,6 +860,25 @@ extern "C" int i8_gemm_tune(int nt, int waves, int mrows, int a_packed, const in
   a.sa = sa; a.sw = sw; a.C = C; a.c_cols = N; a.c_ld = N;
   hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream), nt, waves, mrows);
   return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune");
+}
+
+// Split-K forms: int32 partial slices only (acc_out [kslices][M][N]), packed A;
+// xcd_map as GemmArgs::xcd_map (ignored where the grid does not allow it).
+extern "C" int i8_gemm_tune_sk(int nt, int waves, int mrows, int kslices, int xcd_map,
+                               const int8_t* A, const void* W_packed, int32_t* acc_out, int M,
+                               int N, int K, void* stream) {
+  LLM_REQUIRE(kslices >= 1 && kslices <= 8 && K % 64 == 0 && N % 16 == 0, "i8_gemm_tune_sk: shape");
+  GemmArgs a{};
+  a.a_packed = 1;
+  a.A = reinterpret_cast<const uint8_t*>(A);
+  a.lda = K;
+  a.B = static_cast<const uint8_t*>(W_packed);
+  a.M = M; a.N = N; a.K = K; a.KS = K / 64;
+  a.partial = 1;
+  a.acc_out = acc_out;
+  a.xcd_map = xcd_map;
+  hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream), nt, waves, mrows, kslices);
+  return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune_sk");
 }
 
 // The FP16 GEMM with a forced form (A in packed-A order when a_packed).

@@ -59,6 +59,7 @@ struct WeightGemm {
   // reading LnPartials) sums them and applies the epilogue
   int partial = 0;
   int32_t* acc_out = nullptr;
+  int w_keep = 0;  // weights with the default cache policy (kept in the Infinity Cache), else nt
 };
 
 // Split-K input of a LayerNorm launch: x[m][n] = (float)(sum_z part[z][m][n])

@@ -56,7 +56,8 @@ struct LmHeadArgs {
   int32_t* part_idx;  // [M][nwg]
   int M, V, K, nwg;
   int tiles;  // vocabulary tiles (computing waves) per workgroup, <= kLmWaves
-  int mode;  // 0; tuning build (LLM_LM_MODE): bit0 skip MFMA, bit1 skip x staging, bit2 skip E loads
+  int mode;  // 0; tuning build (LLM_LM_MODE): bit0 skip MFMA, bit1 skip x staging, bit2 skip
+             // E loads; bit3: E with the default cache policy (kept) instead of nt
 };
 
 // MT = 16-row tiles of x per workgroup (1, 2 or 4).
@@ -90,7 +91,8 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
       const int k = c * kLmKChunk + ks * 32;
       const uint32_t off = (e_off == 0xFFFFFFF0u || k >= a.K) ? 0xFFFFFFF0u : e_off + (uint32_t)(k / 32) * 1024u;
       dst[ks] = (a.mode & 4) ? u32x4{0u, 0u, 0u, (uint32_t)ks}
-                             : __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: read once, nt
+                : (a.mode & 8) ? __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 0)  // E kept
+                               : __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: nt
     }
   };
   // Stage x[m0:m0+16MT][c*256 : +256] as hi/lo A fragments: fragment (mt, ks)

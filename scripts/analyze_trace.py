@@ -47,6 +47,16 @@ for t, d in ev:
     act += d
     last = t
 print(f"busy {busy / 1e3:.1f} us, idle {(t1 - t0 - busy) / 1e3:.1f} us, >1 kernel running {multi / 1e3:.1f} us")
+if "--by-position" in sys.argv:
+    # kernels per layer from the step's repeating pattern: position j of each
+    # layer (o_proj and fc2 share a grid; this separates them)
+    names = [re.sub(r"^void |llm::|\(.*$", "", r["Kernel_Name"])[:40] for r in step]
+    per = int(sys.argv[sys.argv.index("--by-position") + 1])
+    body = step[: (len(step) // per) * per]
+    for j in range(per):
+        ds = sorted((r["e"] - r["s"]) / 1e3 for r in body[j::per])
+        g = "x".join(body[j].get(c, "") for c in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z") if body[j].get(c))
+        print(f"  pos {j}: median {ds[len(ds) // 2]:7.2f} us  min {ds[0]:7.2f}  n {len(ds)}  {names[j]} grid={g}")
 if "--dump" in sys.argv:
     for r in step[:80]:
         print(f"{(r['s'] - t0) / 1e3:9.1f} {(r['e'] - r['s']) / 1e3:8.1f} q{r['Queue_Id']} {r['Kernel_Name'][:70]}")
