@@ -104,12 +104,7 @@ struct llm_decoder {
   int tap(int l, int stage, const struct Rows& R, int K, hipStream_t st);
   int layer_norm_into(WeightGemm& g, const struct Rows& R, const float* gamma, const float* beta,
                       hipStream_t st);
-  // split-K o_proj / fc2 (I8 decode): int32 partials in `part`, summed with
-  // the GEMM's epilogue by the next LayerNorm launch (pending describes them)
-  DevBuf<int32_t> part;
-  LnPartials pending;
-  LnPartials embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
-  bool split_k(const struct Rows& R, int N, int K) const;
+  LnSource embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
 
   ~llm_decoder() {
     if (graph) (void)hipGraphExecDestroy(graph);
@@ -204,7 +199,6 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
     d->attn_ws_bytes = std::max(d->attn_ws_bytes,
                                 pa_decode_workspace_bytes(b, d->H, d->D, d->max_tiles, 0));
   RET_IF(d->attn_ws.alloc(std::max<size_t>(d->attn_ws_bytes, 16)));
-  RET_IF(d->part.alloc((size_t)4 * B * hid));  // <= 4 k slices of [B][hid]
   d->qa_ld = std::max(hid, inter);
   // Splitting the rows into two micro-batches on two streams was measured and
   // removed: one graph with two branches, two graphs on two
@@ -399,32 +393,21 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
 int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamma,
                                  const float* beta, hipStream_t st) {
   // the step's first LayerNorm reads the token embedding rows (step_head)
-  const LnPartials src = embed_src.emb ? embed_src : pending;
-  embed_src = LnPartials{};
+  const LnSource src = embed_src;
+  embed_src = LnSource{};
   if (R.prefill_row < 0 && ln_fusable(wdtype, R.n, hid)) {
     g.ln_x = R.x; g.ln_g = gamma; g.ln_b = beta; g.ln_eps = 1e-5f;
     g.ln_emb = src.emb; g.ln_tok = src.tok; g.ln_V = src.V;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
     return LLM_OK;
   }
-  // a pending split-K result is summed (and its rows stored to x) first
-  const LnPartials* pp = src.part || src.emb ? &src : nullptr;
+  const LnSource* pp = src.emb ? &src : nullptr;
   if (wdtype == LLM_I8)
     LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, gamma, beta, 1e-5f, nullptr,
                                        static_cast<int8_t*>(R.act), R.sa, st, 1, pp));
   else
     LLM_HIP_RET(launch_layernorm_f16(R.x, R.n, hid, gamma, beta, 1e-5f, R.act, st, 1, pp));
-  pending = LnPartials{};
   return LLM_OK;
-}
-
-// Split-K for an I8 weight GEMM of N columns whose output feeds a LayerNorm
-// launch (33..64 decode rows; not the GEMM-fused LayerNorm): the column grid
-// alone leaves CUs idle, and every workgroup then reads 1/slices of A.
-bool llm_decoder::split_k(const Rows& R, int N, int K) const {
-  // 17..32 rows take the narrow 16-row tiles instead (gemm.hip narrow_decode_tile)
-  return wdtype == LLM_I8 && R.prefill_row < 0 && R.n > 32 && R.n <= 64 &&
-         !ln_fusable(wdtype, R.n, hid) && gemm_kslices(N, R.n, K / 64) > 1;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
@@ -476,12 +459,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   RET_IF(tap(l, 1, R, hid, st));
   g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = R.x;
   if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
-  if (split_k(R, hid, hid)) {  // partials -> LN2 (x rebuilt there)
-    g.partial = 1; g.acc_out = part.p; g.C = nullptr;
-    pending = LnPartials{part.p, gemm_kslices(hid, R.n, hid / 64), R.sa, g.sw, nullptr, R.x};
-  }
   RET_IF(weight_gemm(g, st));
-  g.partial = 0; g.acc_out = nullptr;
   // LN2 -> mlp_fc1 (+b1, ReLU)
   RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
@@ -507,10 +485,6 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
-  if (l + 1 < L && split_k(R, hid, inter)) {  // partials -> the next layer's LN1
-    g.partial = 1; g.acc_out = part.p; g.C = nullptr; g.bias = nullptr;
-    pending = LnPartials{part.p, gemm_kslices(hid, R.n, inter / 64), R.sa, g.sw, b2.p + lh, R.x};
-  }
   return weight_gemm(g, st);
 }
 
@@ -581,7 +555,7 @@ int llm_decoder::next_tokens(const float* xr, int n, int r0, const int32_t* ctr,
 // (launch or GEMM prologue) reads E[token] rows directly (embed_src).
 int llm_decoder::step_head(hipStream_t st, int r0, int n) {
   (void)st;
-  embed_src = LnPartials{};
+  embed_src = LnSource{};
   embed_src.emb = reinterpret_cast<const _Float16*>(emb.p);
   embed_src.tok = tokens.p + r0;
   embed_src.V = V;
@@ -596,7 +570,6 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
 // One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
   const Rows R = step_rows(0, batch, attn_ws.p);
-  pending = LnPartials{};
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -722,8 +695,7 @@ int llm_decoder::prefill(int row, const int32_t* toks, int n, hipStream_t st) {
     R.prefill_p0 = p0;
     R.attn_ws = pws.p; R.attn_ws_bytes = pws_bytes;
     LLM_HIP_RET(launch_embed(emb.p, pmeta.p + 3 * C, m, hid, V, px.p, st));
-    embed_src = LnPartials{};  // (a failed step enqueue could have left either set)
-    pending = LnPartials{};
+    embed_src = LnSource{};  // (a failed step enqueue could have left it set)
     for (int l = 0; l < L; ++l) {
       RET_IF(layer_pre(l, st, R));
       RET_IF(layer_attn(l, st, R));

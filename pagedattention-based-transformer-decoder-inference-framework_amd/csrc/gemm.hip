@@ -71,15 +71,16 @@ struct GemmArgs {
   float ln_eps;
   uint8_t* act_out;       // optional: workgroups of column block 0 store A (packed-A order)
   float* sa_out;          //   and the I8 row scales (activation taps)
-  // split-K (I8, gridDim.z = k slices): slice z sums k-steps [z KS/Z, (z+1) KS/Z)
-  // and stores its exact int32 partial sums to acc_out + z * M * N ([M][N]),
-  // nothing else; the consumer adds the slices and applies the epilogue.
+  // split-K (I8, gridDim.z = k slices; tuning build only, i8_gemm_tune_sk):
+  // slice z sums k-steps [z KS/Z, (z+1) KS/Z) and stores its exact int32
+  // partial sums to acc_out + z * M * N ([M][N]), nothing else.  The decode
+  // step used it into the LayerNorm launch until round 3 (narrow_decode_tile).
   int partial;
   // 1: weights loaded with the default cache policy (a model whose weights fit
   // the 256 MiB Infinity Cache keeps them there from step to step); 0: nt
   // (streamed once per step, not kept: larger models)
   int w_keep;
-  // split-K only: 1 = workgroups remapped so that slice z runs on XCDs
+  // split-K only (tuning build): 1 = workgroups remapped so that slice z runs on XCDs
   // [z 8/Z, (z+1) 8/Z) (dispatch places linear workgroup i on XCD i % 8), so
   // each XCD's L2 fetches only its slices' A columns instead of all of A
   // (launch_gemm checks 8 % Z == 0 and tiles * Z % 8 == 0)
@@ -231,6 +232,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   const int lane = lane_id();
   const int w = wave_id_uniform();
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+#if LLM_TUNING
   if (a.xcd_map) {
     const int per = 8 / (int)gridDim.z;  // XCDs per k slice
     const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
@@ -240,6 +242,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     bx = tile % (int)gridDim.x;
     by = tile / (int)gridDim.x;
   }
+#endif
   const int nt0 = bx * NT;
   const int m0 = by * 16 * MT;
   unsigned long long* stamp =
@@ -481,10 +484,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       int32_t s = 0;
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) s += red[ww][mt * NT + j][reg][src_lane];
+#if LLM_TUNING
       if (a.partial) {
         a.acc_out[((size_t)bz * a.M + m) * a.N + n] = s;
         continue;
       }
+#endif
       if (a.acc_out) a.acc_out[(size_t)m * a.N + n] = s;
       y = (float)s * e_scale[e];
       if (a.bias) y = y + e_bias[e];
@@ -577,21 +582,14 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t
 template <GemmKind KIND, int MT>
 hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hipStream_t st,
                           int kslices) {
+#if LLM_TUNING
   if (NT == 4 && !a.ln_x) return launch_gemm_nt<KIND, MT, 4>(a, waves, mblocks, st, kslices);
+#endif
   return NT == 2 ? launch_gemm_nt<KIND, MT, 2>(a, waves, mblocks, st, kslices)
                  : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st, kslices);
 }
 
 }  // namespace
-
-// k slices of a split-K launch: enough to give 256 workgroups (the CU count)
-// at one column tile per workgroup, at most 4, each slice >= 8 k-steps.
-int gemm_kslices(int N, int M, int KS) {
-  const int groups = ((N + 15) / 16) * ((M + 63) / 64);
-  int ks = 1;
-  while (ks < 4 && groups * ks < 256 && KS / (2 * ks) >= 8) ks *= 2;
-  return ks;
-}
 
 namespace {
 
@@ -606,12 +604,26 @@ inline int pick_waves(const GemmArgs&, int) { return 8; }
 // --M 32, two runs agree within 0.1 us): qkv 7.0 -> 6.5 us, o_proj 4.8 ->
 // 3.6, fc2 10.1 -> 7.0 (fc1 keeps NT 2 x 32 rows, 7.8).  In the C4 step
 // (same box, scripts/gpu_lib_ab.sh) +3.3..4.1 % over split-K.  At 64 rows
-// (C3) the same forms lost 0.3 % to split-K, which stays there.
+// (C3) the same forms lost 0.3 % to split-K.
+// Decode rows 33..64 (C3), column grid under 256 tiles (o_proj, fc2 at hid
+// 2048): 2 column tiles x 16 rows x 8 waves, four row blocks each streaming
+// the weights (the repeats from L2 / the Infinity Cache).  Round 3 sweep of
+// every (NT 1/2/4, waves, rows, k slices, XCD placement) form
+// (scripts/tune_gemm_sk.py): o_proj 5.39 -> 4.74 us, fc2 9.74 -> 8.90 us
+// against split-K 2 into the LayerNorm; in the C3 step (same box,
+// scripts/gpu_lib_ab.sh, two rounds) 3,741 / 3,744 -> 3,811 / 3,802 tok/s,
+// the LayerNorm launches also reading one fp32 row instead of two int32 slices.
+// That retired split-K from the decode step (the tuning build keeps it).
 struct TileChoice {
   int nt, waves, mrows;
 };
 inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
-  if (a.ln_x || a.partial || a.M <= 16 || a.M > 32) return false;
+  if (a.ln_x || a.partial || a.M <= 16 || a.M > 64) return false;
+  if (a.M > 32) {
+    if ((a.N + 15) / 16 >= 256) return false;
+    t = TileChoice{2, 8, 16};
+    return true;
+  }
   const int ntiles = (a.N + 15) / 16;
   const int K = a.KS * kstep;
   if (ntiles < 384) {
@@ -648,7 +660,7 @@ hipError_t launch_gemm(const GemmArgs& a_in, hipStream_t st, int nt_override = 0
   // Infinity Cache); split-K fills them with k slices instead
   if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256 && !a.ln_x && !a.partial) mrows = 32;
   if (mrows_override > 0) mrows = mrows_override;
-  const int ks = !a.partial ? 1 : ks_override > 0 ? ks_override : gemm_kslices(a.N, a.M, a.KS);
+  const int ks = a.partial ? std::max(1, ks_override) : 1;
   const int mblocks = (a.M + mrows - 1) / mrows;
   const int tiles = ((a.N + 15) / 16 + NT - 1) / NT * mblocks;
   if (a.xcd_map && (ks < 2 || 8 % ks != 0 || (tiles * ks) % 8 != 0)) a.xcd_map = 0;
@@ -776,12 +788,6 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;
   a.w_keep = g.w_keep;
-  if (g.partial) {
-    LLM_REQUIRE(g.dtype == LLM_I8 && g.acc_out && !g.ln_x && !g.kv && !g.C16,
-                "weight_gemm: split-K is an I8 GEMM writing only int32 partials");
-    a.partial = 1;
-    a.acc_out = g.acc_out;
-  }
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");

@@ -54,26 +54,12 @@ struct WeightGemm {
   float ln_eps = 1e-5f;
   void* act_out = nullptr;
   float* sa_out = nullptr;
-  // split-K (I8): k slices (gemm_kslices) write exact int32 partial sums to
-  // acc_out [slices][M][N] and nothing else; the consumer (a LayerNorm launch
-  // reading LnPartials) sums them and applies the epilogue
-  int partial = 0;
-  int32_t* acc_out = nullptr;
   int w_keep = 0;  // weights with the default cache policy (kept in the Infinity Cache), else nt
 };
 
-// Split-K input of a LayerNorm launch: x[m][n] = (float)(sum_z part[z][m][n])
-// * (sa[m] * sw[n]) + bias[n] -- bit for bit the GEMM epilogue it replaces.
-// Input of the LayerNorm launch when it is not x: a split-K GEMM's int32
-// partials (part != NULL), or embedding rows E[tok[r]] (emb != NULL; the
-// decode step's first LayerNorm reads the token embedding directly).
-struct LnPartials {
-  const int32_t* part = nullptr;
-  int slices = 0;
-  const float* sa = nullptr;
-  const float* sw = nullptr;
-  const float* bias = nullptr;  // may be NULL
-  float* x_out = nullptr;       // the reconstructed rows (fp32 [M][N])
+// Input of a LayerNorm when it is not x: embedding rows E[tok[r]] (the decode
+// step's first LayerNorm reads the token embedding directly, no embed launch).
+struct LnSource {
   const _Float16* emb = nullptr;
   const int32_t* tok = nullptr;
   int V = 0;
@@ -83,7 +69,5 @@ int weight_gemm(const WeightGemm& g, hipStream_t st);
 // Whether weight_gemm can run the LayerNorm prologue for M rows of K (the
 // per-workgroup A image must fit in LDS; K <= 128 groups of 16 bytes).
 bool ln_fusable(int dtype, int M, int K);
-// k slices weight_gemm uses for a split-K launch of N columns, M rows, KS k-steps
-int gemm_kslices(int N, int M, int KS);
 
 }  // namespace llm

@@ -165,62 +165,25 @@ __global__ __launch_bounds__(kRowThreads) void quantize_rows_v_kernel(
 }
 
 // LayerNorm (+ int8 quantisation) launch, one 256-thread workgroup per row:
-// every thread loads its VPT float4 chunks (chunk c = threadIdx.x + 256 v) --
-// of x, or of a split-K GEMM's int32 partial slices plus that GEMM's scales
-// and bias (pp.part, LnPartials: the row is rebuilt with the GEMM's epilogue
-// and stored to pp.x_out) -- and gamma / beta, all in ONE memory round trip;
+// every thread loads its VPT float4 chunks (chunk c = threadIdx.x + 256 v) of
+// x (or of the embedding row E[tok[r]], pp.emb) and gamma / beta, all in ONE
+// memory round trip;
 // wave DPP sums + one LDS exchange per reduction.  Numerics of
 // LayerNorm<T>::forward (decoder/layer_norm.hpp:20-37) and int8_quant.cpp as
 // ln_wave.hpp (the GEMM prologue); only the fp32 summation order differs.
 // q / out16 in packed-A order when pack.
-// inv_scale is NOT __restrict__: with split-K partials pp.sa (the GEMM's row
-// scales) is the same buffer the row's new scale is written to; every read of
-// pp.sa comes before the block reductions that the write depends on.
 template <int VPT>
 __global__ __launch_bounds__(kRowThreads) void layernorm_rows_kernel(
     const float* __restrict__ x, int rows, int cols, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
-    float* inv_scale, _Float16* __restrict__ out16, int pack, LnPartials pp) {
+    float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack, LnSource pp) {
   __shared__ float sh[4];
   const int r = blockIdx.x;
   const int n4 = cols >> 2;
   const f32x4* g4 = reinterpret_cast<const f32x4*>(gamma);
   const f32x4* b4 = reinterpret_cast<const f32x4*>(beta);
   f32x4 v[VPT], gv[VPT], bv[VPT];
-  bool from_partials = false;
-  if constexpr (VPT <= 4) from_partials = pp.part != nullptr;  // (launch_ln checks)
-  if (from_partials) {
-    constexpr int kMaxSlices = 4;
-    i32x4 pv[kMaxSlices][VPT];
-    f32x4 sw[VPT], bi[VPT];
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = threadIdx.x + i * kRowThreads;
-      const bool ok = c < n4;
-#pragma unroll
-      for (int z = 0; z < kMaxSlices; ++z)
-        pv[z][i] = ok && z < pp.slices
-                       ? reinterpret_cast<const i32x4*>(pp.part + ((size_t)z * rows + r) * cols)[c]
-                       : i32x4{0, 0, 0, 0};
-      sw[i] = ok ? reinterpret_cast<const f32x4*>(pp.sw)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-      bi[i] = ok && pp.bias ? reinterpret_cast<const f32x4*>(pp.bias)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-      gv[i] = ok ? g4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-      bv[i] = ok ? b4[c] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const float sa = pp.sa[r];
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const i32x4 acc = (pv[0][i] + pv[1][i]) + (pv[2][i] + pv[3][i]);  // exact
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {  // the GEMM epilogue: acc * (sa * sw), then + bias
-        float y = __fmul_rn((float)acc[e], __fmul_rn(sa, sw[i][e]));
-        if (pp.bias) y = __fadd_rn(y, bi[i][e]);
-        v[i][e] = y;
-      }
-      const int c = threadIdx.x + i * kRowThreads;
-      if (pp.x_out && c < n4) reinterpret_cast<f32x4*>(pp.x_out + (size_t)r * cols)[c] = v[i];
-    }
-  } else if (pp.emb) {  // x = E[tok[r]] (embed_kernel's values, not stored)
+  if (pp.emb) {  // x = E[tok[r]] (embed_kernel's values, not stored)
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     const h4* er = reinterpret_cast<const h4*>(ln_embed_row(pp.emb, pp.tok, r, pp.V, cols));
 #pragma unroll
@@ -417,10 +380,9 @@ hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, f
 
 static hipError_t launch_ln(const float* x, int rows, int cols, const float* g, const float* b,
                             float eps, float* out, int8_t* q, float* inv, _Float16* out16,
-                            hipStream_t st, int pack, const LnPartials* pp = nullptr) {
-  const LnPartials none{};
+                            hipStream_t st, int pack, const LnSource* pp = nullptr) {
+  const LnSource none{};
   const int v = row_vpt(cols);
-  if (pp && pp->part && (v == 0 || v > 4 || pp->slices > 4)) return hipErrorInvalidValue;
   if (pack && (v == 0 || cols % 64 != 0)) return hipErrorInvalidValue;
   if (pp && pp->emb && v == 0) return hipErrorInvalidValue;
   if (v == 0) {  // odd widths (C ABI only)
@@ -442,13 +404,13 @@ static hipError_t launch_ln(const float* x, int rows, int cols, const float* g, 
 
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
-                                  hipStream_t st, int pack, const LnPartials* pp) {
+                                  hipStream_t st, int pack, const LnSource* pp) {
   return launch_ln(x, rows, cols, g, b, eps, out, q, inv, nullptr, st, pack, pp);
 }
 
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
                                 const float* b, float eps, void* out16, hipStream_t st, int pack,
-                                const LnPartials* pp) {
+                                const LnSource* pp) {
   return launch_ln(x, rows, cols, g, b, eps, nullptr, nullptr, nullptr,
                    static_cast<_Float16*>(out16), st, pack, pp);
 }

@@ -12,15 +12,15 @@ namespace llm {
 // needs cols % 64 == 0), consumed by the weight GEMMs with a_packed.
 hipError_t launch_quantize_rows(const float* x, int rows, int cols, int8_t* q, float* inv,
                                 hipStream_t st, int pack = 0);
-struct LnPartials;
-// pp (optional): rebuild x from a split-K GEMM's int32 partials first, or read
-// the rows as embedding rows E[tok[r]] (gemm.hpp LnPartials)
+struct LnSource;
+// pp (optional): read the rows as embedding rows E[tok[r]] instead of x
+// (gemm.hpp LnSource)
 hipError_t launch_layernorm_quant(const float* x, int rows, int cols, const float* g,
                                   const float* b, float eps, float* out, int8_t* q, float* inv,
-                                  hipStream_t st, int pack = 0, const LnPartials* pp = nullptr);
+                                  hipStream_t st, int pack = 0, const LnSource* pp = nullptr);
 hipError_t launch_layernorm_f16(const float* x, int rows, int cols, const float* g,
                                 const float* b, float eps, void* out16, hipStream_t st,
-                                int pack = 0, const LnPartials* pp = nullptr);
+                                int pack = 0, const LnSource* pp = nullptr);
 hipError_t launch_to_f16(const float* x, size_t n, void* y, hipStream_t st, int pack_cols = 0);
 hipError_t launch_advance(int32_t* pos, int32_t* ctx, int n, hipStream_t st);
 hipError_t launch_argmax(const float* logits, int rows, int V, int32_t* out, int32_t* out2,

@@ -683,13 +683,12 @@ def test_forced_step_48_rows(gpu, oracle):
 
 
 @pytest.mark.parametrize("rows", [24, 48])
-def test_forced_split_k_hidden_2048(gpu, oracle, rows):
+def test_forced_hidden_2048_tile_forms(gpu, oracle, rows):
     """hid 2048: the LayerNorms are launches (the rows' fp32 image is too big
-    for the GEMM prologue).  At 48 rows o_proj and the non-final fc2 run
-    split-K (two k slices of exact int32 partials, summed with the GEMM's
-    epilogue by the next LayerNorm launch); at 24 rows the GEMMs take the
-    narrow 16-row tiles (two row blocks, 4-wave workgroups for K < 4096).
-    Teacher forced, north_star bar."""
+    for the GEMM prologue).  At 48 rows o_proj and fc2 run 2-column-tile
+    16-row workgroups (three row blocks; round 2 ran split-K here); at 24 rows
+    the GEMMs take the narrow 16-row tiles (two row blocks, 4-wave workgroups
+    for K < 4096).  Teacher forced, north_star bar."""
     from oracle.oracle import OracleDecoder
     w = _int8_model(oracle, L=2, H=16, D=128, V=512, S=24, seed=41)
     dec = _make_gpu_decoder(w, max_batch=rows)

@@ -24,6 +24,8 @@ def _dev(a):
     (512, 2048, 2048), (300, 512, 256), (256, 8192, 512), (513, 1024, 96),
     # 17..32 rows: the 16-row tile forms (narrow_decode_tile), every output class
     (17, 2048, 2048), (24, 2048, 6144), (32, 8192, 2048), (32, 2048, 8192), (20, 768, 768),
+    # 33..64 rows, under 256 column tiles: 2 column tiles x 16-row workgroups
+    (33, 2048, 2048), (48, 8192, 2048), (64, 2048, 2048), (40, 768, 2304),
 ])
 def test_i8_gemm_exact(gpu, oracle, M, K, N):
     import llm_capi
@@ -58,7 +60,7 @@ def test_i8_gemm_no_scales(gpu, oracle):
 
 @pytest.mark.parametrize("M,K,N,nt,waves", [
     (64, 2048, 6144, 2, 8), (64, 8192, 2048, 1, 8), (64, 2048, 2048, 1, 16), (37, 512, 96, 2, 8),
-    (16, 256, 64, 1, 8), (100, 1024, 512, 2, 16),
+    (16, 256, 64, 1, 8), (100, 1024, 512, 2, 16), (64, 8192, 2048, 4, 4), (48, 2048, 2048, 4, 8),
     (512, 1024, 768, 0, 0), (300, 512, 4096, 0, 0),  # prefill-chunk row counts
 ])
 def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
@@ -90,6 +92,34 @@ def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
                                             Wp.data_ptr(), C.data_ptr(), M, N, K, dsa.data_ptr(),
                                             dsw.data_ptr(), None), lib)
             np.testing.assert_array_equal(C.cpu().numpy(), ref_C)
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 2048, 2048), (32, 8192, 2048), (45, 1024, 256)])
+def test_i8_gemm_split_k_forms_exact(gpu, oracle, M, K, N):
+    """The tuning build's split-K forms (i8_gemm_tune_sk: 1-8 k slices of
+    exact int32 partials, 1/2/4 column tiles, with and without the XCD-aware
+    slice placement): the slices sum to the oracle's int32 product exactly."""
+    import ctypes
+    import torch
+    import llm_capi
+    lib = llm_capi.load_tune()
+    lib.i8_gemm_tune_sk.restype = ctypes.c_int
+    lib.i8_gemm_tune_sk.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p]
+    rng = np.random.default_rng(M + K + N)
+    A = rng.integers(-128, 128, (M, K), dtype=np.int8)
+    W = rng.integers(-128, 128, (K, N), dtype=np.int8)
+    Wp = llm_capi.pack_weights(_dev(W), llm_capi.LLM_I8)
+    Ap = llm_capi.pack_weights(_dev(np.ascontiguousarray(A.T)), llm_capi.LLM_I8)
+    ref = A.astype(np.int64) @ W.astype(np.int64)
+    part = torch.empty((8, M, N), dtype=torch.int32, device="cuda")
+    for nt, waves, mrows, ks, xcd in ((1, 8, 64, 2, 0), (1, 8, 64, 2, 1), (2, 8, 16, 4, 1),
+                                      (4, 4, 32, 8, 1), (2, 4, 16, 1, 0), (1, 8, 32, 8, 0)):
+        part.fill_(-7)
+        llm_capi.check(lib.i8_gemm_tune_sk(nt, waves, mrows, ks, xcd, Ap.data_ptr(), Wp.data_ptr(),
+                                           part.data_ptr(), M, N, K, None), lib)
+        got = part[:ks].to(torch.int64).sum(0).cpu().numpy()
+        np.testing.assert_array_equal(got, ref, err_msg=str((nt, waves, mrows, ks, xcd)))
 
 
 @pytest.mark.parametrize("M,K,N", [(16, 768, 2304), (64, 2048, 512), (3, 96, 48), (80, 256, 64),
