@@ -58,7 +58,7 @@ def main():
     d = Path(sys.argv[1])
     tr = by_role(gemm_dispatches(d / "trace", "*kernel_trace.csv", False))
     cn = {s: by_role(gemm_dispatches(d / s, "*counter_collection.csv", True))
-          for s in ("mfma", "mops", "fetch")}
+          for s in ("mfma", "mops", "fetch", "write")}
     res = {"config": "C3 INT8 decoder, 64 rows, eager steps (scripts/prof_gemm.py)",
            "peaks": {"int8_mfma_ops_per_s": PEAK_OPS, "hbm_bytes_per_s": PEAK_BW},
            "gemms": {}}
@@ -70,6 +70,7 @@ def main():
         mops = med([e.get("SQ_INSTS_VALU_MFMA_MOPS_I8", 0) for e in cn["mops"][role]])
         busy = med([e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) for e in cn["mfma"][role]])
         fetch = med([e.get("FETCH_SIZE", 0) for e in cn["fetch"][role]])
+        write = med([e.get("WRITE_SIZE", 0) for e in cn["write"][role]]) if cn["write"][role] else None
         ops = 2.0 * M * K * N
         wbytes = K * N + 4 * N  # int8 weights + fp32 column scales
         ent = {"kernel": kern, "M": M, "K": K, "N": N, "dispatches": len(tr[role]),
@@ -83,6 +84,19 @@ def main():
                "weight_GBps": round(wbytes / t / 1e9, 1),
                "hbm_frac_vs_8TBps": round(wbytes / t / PEAK_BW, 4),
                "hbm_bytes_pmc": int(2 * fetch * 1024) if fetch else None}
+        # attribution: weights once; A (int8 M x K + row scales) once per XCD
+        # (every XCD runs workgroups of every row block); output fp32 (qkv: q
+        # fp32 + K / V fp16 into the pages)
+        a_bytes = M * K + 4 * M
+        out_b = M * (K * 4 + 2 * K * 2) if role == "qkv" else M * N * 4
+        ent["attribution"] = {
+            "weights_B": wbytes, "A_B": a_bytes, "A_xcd_fetches": 8, "output_B": out_b,
+            "fetch_model_B": wbytes + 8 * a_bytes,
+            "fetch_pmc_over_model": round(2 * fetch * 1024 / (wbytes + 8 * a_bytes), 3) if fetch else None,
+            "write_B_pmc": int(write * 1024) if write else None,
+            "write_pmc_over_output": round(write * 1024 / out_b, 3) if write else None,
+            "pmc_over_unique": round((2 * fetch + (write or 0)) * 1024 / (wbytes + a_bytes + out_b), 3)
+            if fetch else None}
         res["gemms"][role] = ent
         tot_t += t
         tot_w += wbytes

@@ -14,4 +14,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
 timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/mfma -o mfma -- python3 $R/scripts/prof_gemm.py > $O/mfma.log 2>&1 || exit 1
 timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_I8 --kernel-trace --output-format csv -d $O/mops -o mops -- python3 $R/scripts/prof_gemm.py > $O/mops.log 2>&1 || echo "MOPS_I8 pass failed"
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o fetch -- python3 $R/scripts/prof_gemm.py > $O/fetch.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o write -- python3 $R/scripts/prof_gemm.py > $O/write.log 2>&1 || exit 1
 cd $R && python3 scripts/gemm_pmc_summarize.py $O > $O/summary.json && cat $O/summary.json
