@@ -43,8 +43,7 @@ namespace llm {
 // workgroup = 242 workgroups on 256 CUs, where 16 left 59 CUs idle (197
 // workgroups of 1 MiB of E each at C3).  At least 8, so small vocabularies do
 // not stage x once per tile.
-constexpr int kLmWaves = 16;
-constexpr int kLmThreads = 64 * kLmWaves;
+constexpr int kLmWaves = 16;            // vocabulary tiles per workgroup <= 16
 constexpr int kLmKChunk = 256;          // K per LDS stage (8 k-steps of 32)
 constexpr int kLmKs = kLmKChunk / 32;
 
@@ -60,40 +59,53 @@ struct LmHeadArgs {
              // E loads; bit3: E with the default cache policy (kept) instead of nt
 };
 
-// MT = 16-row tiles of x per workgroup (1, 2 or 4).
-template <int MT>
-__global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
+// MT = 16-row tiles of x per workgroup (1, 2 or 4); WAVES waves, each NTW
+// vocabulary tiles (16 rows of E) per k-step against one read of the x
+// fragments from LDS.
+template <int MT, int WAVES, int NTW>
+__global__ __launch_bounds__(WAVES * 64) void lm_head_kernel(LmHeadArgs a) {
+  constexpr int kLmThreads = WAVES * 64;
   // A fragments of the chunk: [mt][ks][hi/lo][64 lanes] x 16 B
   __shared__ __attribute__((aligned(16))) u32x4 xa[MT][kLmKs][2][64];
-  __shared__ float pv[kLmWaves][16 * MT];
-  __shared__ int pi[kLmWaves][16 * MT];
+  __shared__ float pv[WAVES * NTW][16 * MT];
+  __shared__ int pi[WAVES * NTW][16 * MT];
   const int lane = lane_id();
   const int w = wave_id_uniform();
   const int m0 = blockIdx.y * 16 * MT;
-  const int ntile = blockIdx.x * a.tiles + w;  // this wave's 16 vocabulary rows
-  const int n0 = ntile * 16;
-  const bool mine = w < a.tiles;  // a wave past `tiles` only stages x
   const int KS = a.K / 32;
   const int ntiles = (a.V + 15) / 16;
   const auto ers = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.E, (short)0, (uint32_t)min((size_t)ntiles * KS * 1024, (size_t)0xFFFFFFF0u), 0x00020000);
-  const uint32_t e_off =
-      mine && ntile < ntiles ? (uint32_t)((size_t)ntile * KS * 1024) + lane * 16 : 0xFFFFFFF0u;
-
-  f32x4 acc[MT];
+  // wave w's tiles: w * NTW + j of the workgroup's `tiles` (a wave past them only stages x)
+  uint32_t e_off[NTW];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NTW; ++j) {
+    const int t = w * NTW + j;
+    const int ntile = blockIdx.x * a.tiles + t;
+    e_off[j] = t < a.tiles && ntile < ntiles ? (uint32_t)((size_t)ntile * KS * 1024) + lane * 16
+                                             : 0xFFFFFFF0u;
+  }
+  const bool mine = w * NTW < a.tiles;
+
+  f32x4 acc[NTW][MT];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[j][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = (a.K + kLmKChunk - 1) / kLmKChunk;  // K % 32 == 0; tail k-steps load 0
-  auto issue = [&](u32x4 (&dst)[kLmKs], int c) {
+  auto issue = [&](u32x4 (&dst)[NTW][kLmKs], int c) {
 #pragma unroll
-    for (int ks = 0; ks < kLmKs; ++ks) {
-      const int k = c * kLmKChunk + ks * 32;
-      const uint32_t off = (e_off == 0xFFFFFFF0u || k >= a.K) ? 0xFFFFFFF0u : e_off + (uint32_t)(k / 32) * 1024u;
-      dst[ks] = (a.mode & 4) ? u32x4{0u, 0u, 0u, (uint32_t)ks}
-                : (a.mode & 8) ? __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 0)  // E kept
-                               : __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: nt
-    }
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int ks = 0; ks < kLmKs; ++ks) {
+        const int k = c * kLmKChunk + ks * 32;
+        const uint32_t off =
+            (e_off[j] == 0xFFFFFFF0u || k >= a.K) ? 0xFFFFFFF0u : e_off[j] + (uint32_t)(k / 32) * 1024u;
+        dst[j][ks] = (a.mode & 4) ? u32x4{0u, 0u, 0u, (uint32_t)ks}
+                     : (a.mode & 8) ? __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 0)  // E kept
+                                    : __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: nt
+      }
   };
   // Stage x[m0:m0+16MT][c*256 : +256] as hi/lo A fragments: fragment (mt, ks)
   // lane l holds row mt*16 + (l&15), k = ks*32 + 8*(l>>4) .. +8.  Each thread
@@ -139,7 +151,7 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
   // One chunk: stage x, then multiply while the next chunk's E and x loads are
   // in flight.  The two E buffers are distinct named arrays (static register
   // indexing: a dynamically indexed register array would live in scratch).
-  auto chunk = [&](const u32x4 (&cur)[kLmKs], u32x4 (&nxt)[kLmKs], int c) {
+  auto chunk = [&](const u32x4 (&cur)[NTW][kLmKs], u32x4 (&nxt)[NTW][kLmKs], int c) {
     store_x();
     __syncthreads();
     if (c + 1 < nchunks) {
@@ -149,24 +161,29 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
     if (!mine) {
       // stages x only
     } else if (a.mode & 1) {
-      acc[0][0] += __builtin_bit_cast(float, cur[0][0] ^ cur[kLmKs - 1][3]) * 0.f +
-                   (float)xa[0][0][0][lane][0];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        acc[j][0][0] += __builtin_bit_cast(float, cur[j][0][0] ^ cur[j][kLmKs - 1][3]) * 0.f +
+                        (float)xa[0][0][0][lane][0];
     } else {
 #pragma unroll
       for (int ks = 0; ks < kLmKs; ++ks) {
-        const f16x8 bb = __builtin_bit_cast(f16x8, cur[ks]);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const f16x8 hi = __builtin_bit_cast(f16x8, xa[mt][ks][0][lane]);
           const f16x8 lo = __builtin_bit_cast(f16x8, xa[mt][ks][1][lane]);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bb, acc[mt], 0, 0, 0);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bb, acc[mt], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) {
+            const f16x8 bb = __builtin_bit_cast(f16x8, cur[j][ks]);
+            acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bb, acc[j][mt], 0, 0, 0);
+            acc[j][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bb, acc[j][mt], 0, 0, 0);
+          }
         }
       }
     }
     __syncthreads();  // xa is rewritten by the next chunk
   };
-  u32x4 eA[kLmKs], eB[kLmKs];
+  u32x4 eA[NTW][kLmKs], eB[NTW][kLmKs];
   issue(eA, 0);
   load_x(0);
   for (int c = 0; c < nchunks; c += 2) {
@@ -174,15 +191,19 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
     if (c + 1 < nchunks) chunk(eB, eA, c + 1);
   }
 
-  // acc[mt] lane l, reg r: x row m0 + mt*16 + 4*(l>>4) + r, vocab row n0 + (l&15)
-  // (C/D layout: col = lane&15 -> here the vocabulary index, row = 4*(lane>>4)+reg).
-  const int n = mine ? n0 + (lane & 15) : a.V;  // a staging-only wave stores nothing
+  // acc[j][mt] lane l, reg r: x row m0 + mt*16 + 4*(l>>4) + r, vocab row
+  // 16 tile_j + (l&15) (C/D layout: col = lane&15 -> here the vocabulary
+  // index, row = 4*(lane>>4)+reg).
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+  const int t = w * NTW + j;
+  const int n = t < a.tiles ? (blockIdx.x * a.tiles + t) * 16 + (lane & 15) : a.V;  // staging-only: none
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = mt * 16 + 4 * (lane >> 4) + r;
-      const float v = acc[mt][r];
+      const float v = acc[j][mt][r];
       if (a.logits && m0 + row < a.M && n < a.V) a.logits[(size_t)(m0 + row) * a.V + n] = v;
       if (a.part_val) {
         // max over this wave's 16 vocabulary rows (lanes sharing lane>>4), first index on ties
@@ -194,9 +215,10 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
           const int oi = __shfl_xor(bi, off, 64);
           if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
         }
-        if ((lane & 15) == 0) { pv[w][row] = bv; pi[w][row] = bi; }
+        if ((lane & 15) == 0 && t < WAVES * NTW) { pv[t][row] = bv; pi[t][row] = bi; }
       }
     }
+  }
   }
   if (!a.part_val) return;
   __syncthreads();
@@ -204,7 +226,7 @@ __global__ __launch_bounds__(kLmThreads) void lm_head_kernel(LmHeadArgs a) {
     if (m0 + row >= a.M) continue;
     float bv = pv[0][row];
     int bi = pi[0][row];
-    for (int ww = 1; ww < a.tiles; ++ww)  // waves cover increasing vocabulary rows
+    for (int ww = 1; ww < a.tiles; ++ww)  // tiles in increasing vocabulary order
       if (pv[ww][row] > bv) { bv = pv[ww][row]; bi = pi[ww][row]; }
     a.part_val[(size_t)(m0 + row) * a.nwg + blockIdx.x] = bv;
     a.part_idx[(size_t)(m0 + row) * a.nwg + blockIdx.x] = bi;
@@ -324,10 +346,22 @@ hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, i
   LmHeadArgs a{x, static_cast<const _Float16*>(E), logits, part_val, part_idx, M, V, K,
                lm_head_workgroups(V), lm_head_tiles(V), mode};
   const int mt = M <= 16 ? 1 : M <= 32 ? 2 : 4;
-  const dim3 grid(a.nwg, (M + 16 * mt - 1) / (16 * mt)), block(kLmThreads);
-  if (mt == 1) hipLaunchKernelGGL(lm_head_kernel<1>, grid, block, 0, st, a);
-  else if (mt == 2) hipLaunchKernelGGL(lm_head_kernel<2>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(lm_head_kernel<4>, grid, block, 0, st, a);
+  const dim3 grid(a.nwg, (M + 16 * mt - 1) / (16 * mt));
+  // 16 waves x 1 vocabulary tile.  The tuning build's LLM_LM_FORM=1 (8 waves x
+  // 2 tiles: the x fragments read from LDS once per 2 tiles) measured slower
+  // at every row count (C3 / C4 / C2 shapes 58.7 / 46.1 / 16.3 vs 56.0 / 43.8 /
+  // 15.9 us, profiles/r03/lm_head_forms.txt): the LDS reads do not bound it.
+#if LLM_TUNING
+  if (env_int("LLM_LM_FORM", 0)) {
+    if (mt == 1) hipLaunchKernelGGL((lm_head_kernel<1, 8, 2>), grid, dim3(512), 0, st, a);
+    else if (mt == 2) hipLaunchKernelGGL((lm_head_kernel<2, 8, 2>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((lm_head_kernel<4, 8, 2>), grid, dim3(512), 0, st, a);
+    return hipGetLastError();
+  }
+#endif
+  if (mt == 1) hipLaunchKernelGGL((lm_head_kernel<1, 16, 1>), grid, dim3(1024), 0, st, a);
+  else if (mt == 2) hipLaunchKernelGGL((lm_head_kernel<2, 16, 1>), grid, dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL((lm_head_kernel<4, 16, 1>), grid, dim3(1024), 0, st, a);
   return hipGetLastError();
 }
 
