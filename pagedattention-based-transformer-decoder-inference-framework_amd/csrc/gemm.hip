@@ -85,6 +85,10 @@ struct GemmArgs {
   // each XCD's L2 fetches only its slices' A columns instead of all of A
   // (launch_gemm checks 8 % Z == 0 and tiles * Z % 8 == 0)
   int xcd_map;
+  // seam experiment (tuning build, gemm_pair_f16_kernel): arrival counter the
+  // LayerNorm-prologue tile waits on after issuing its first weight batches
+  unsigned* seam;
+  int seam_n;
 };
 
 // LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
@@ -203,8 +207,29 @@ __device__ __forceinline__ void ln_prologue(const GemmArgs& a, int m0, uint8_t* 
   }
 }
 
-template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0>
-__global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
+// One workgroup's tile (column block bx, row block by, k slice bz of nz);
+// gx = column blocks in the grid (diagnostic stamps only).
+// Wait (one lane, relaxed polls with s_sleep, then an acquire fence; the
+// workgroup barrier after it orders every wave's loads) until *ctr >= n.
+// Bounded: a timeout sets ctr[2] and runs on; it never hangs.
+__device__ __forceinline__ void seam_wait(unsigned* ctr, int n) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)n) {
+      __builtin_amdgcn_s_sleep(8);
+      if (++spins > (1u << 21)) {
+        __hip_atomic_store(&ctr[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0, int SEAM = 0>
+__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int bz, int nz,
+                                          int gx) {
   using Tr = GemmTraits<KIND>;
   using acc_t = typename Tr::acc_t;
   constexpr int KSTEP = Tr::KSTEP;
@@ -231,29 +256,17 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
 
   const int lane = lane_id();
   const int w = wave_id_uniform();
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-#if LLM_TUNING
-  if (a.xcd_map) {
-    const int per = 8 / (int)gridDim.z;  // XCDs per k slice
-    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    const int xcd = lin & 7;
-    const int tile = (lin >> 3) * per + xcd % per;
-    bz = xcd / per;
-    bx = tile % (int)gridDim.x;
-    by = tile / (int)gridDim.x;
-  }
-#endif
   const int nt0 = bx * NT;
   const int m0 = by * 16 * MT;
   unsigned long long* stamp =
-      a.stamps ? a.stamps + ((size_t)by * gridDim.x + bx) * 48 : nullptr;
+      a.stamps ? a.stamps + ((size_t)by * gx + bx) * 48 : nullptr;
   if (stamp && lane == 0) stamp[w] = phase_clock();  // [0, 16): wave start
   // Wave w streams k range wr = (w + bx) % WAVES: at any moment the
   // workgroups of an XCD read different A fragments (all of them read all of
   // A), instead of every workgroup hitting the same L2 lines.
   const int wr = (w + bx) % WAVES;
-  const int kz0 = (int)((bz * a.KS) / (int)gridDim.z);  // this k slice (split-K)
-  const int kzn = (int)(((bz + 1) * a.KS) / (int)gridDim.z) - kz0;
+  const int kz0 = (int)((bz * a.KS) / nz);  // this k slice (split-K)
+  const int kzn = (int)(((bz + 1) * a.KS) / nz) - kz0;
   const int ks0 = kz0 + (wr * kzn) / WAVES;
   const int ks1 = kz0 + ((wr + 1) * kzn) / WAVES;
   const int ntiles = (a.N + 15) >> 4;
@@ -388,6 +401,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
       issue(b1, ks0 + kUnroll, false, true);
       b1_pre = true;
     }
+    if constexpr (SEAM != 0) seam_wait(a.seam, a.seam_n);  // weights already in flight
     ln_prologue<KIND, ROWS_, WAVES>(a, m0, alds, sa_lds);
     __syncthreads();
     if constexpr (KIND == GemmKind::I8) {
@@ -512,6 +526,23 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     }
   }
   if (stamp && lane == 0) stamp[32 + w] = phase_clock();  // [32, 48): wave end
+}
+
+template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0>
+__global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+#if LLM_TUNING
+  if (a.xcd_map) {
+    const int per = 8 / (int)gridDim.z;  // XCDs per k slice
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = lin & 7;
+    const int tile = (lin >> 3) * per + xcd % per;
+    bz = xcd / per;
+    bx = tile % (int)gridDim.x;
+    by = tile / (int)gridDim.x;
+  }
+#endif
+  gemm_tile<KIND, MT, NT, WAVES, DIAG, PRO>(a, bx, by, bz, (int)gridDim.z, (int)gridDim.x);
 }
 
 // Repack W [K][N] (row-major) into per-(16-col tile, k-step) 1 KiB blocks,
@@ -885,6 +916,79 @@ extern "C" int i8_gemm_tune_sk(int nt, int waves, int mrows, int kslices, int xc
   a.xcd_map = xcd_map;
   hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream), nt, waves, mrows, kslices);
   return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune_sk");
+}
+
+// Seam experiment (round 3, the C2 verdict item): o_proj -> LN2 + fc1 of the
+// FP16 decoder at <= 16 rows as ONE launch, workgroups 0..n1-1 computing the
+// o_proj tiles, then every workgroup waiting on a device-scope arrival counter
+// (release fence + agent-scope add; relaxed poll with s_sleep, bounded: a
+// timeout sets sync[2] and runs on, it never hangs) before its fc1 tile with
+// the LayerNorm prologue.  sync[0..2] self-reset (the last departing
+// workgroup clears them).  Against the decoder's two launches of the same
+// tile forms: f16_gemm_pair_tune(fused = 0 / 1).
+__global__ __launch_bounds__(512) void gemm_pair_f16_kernel(GemmArgs a1, GemmArgs a2, int n1,
+                                                            unsigned* sync) {
+  const int wg = blockIdx.x;
+  if (wg < n1) {
+    gemm_tile<GemmKind::F16, 1, 1, 8, 0, 0>(a1, wg, 0, 0, 1, n1);
+    // every wave's stores done (the barrier waits on them), then ONE release
+    // fence for the workgroup (one per wave: 19.2 us per pair) and the add
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_fetch_add(&sync[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // fc1 tile: its first weight batches issued, then seam_wait, then the
+  // LayerNorm prologue reads the o_proj rows
+  gemm_tile<GemmKind::F16, 1, 1, 8, 0, 1, 1>(a2, wg, 0, 0, 1, (int)gridDim.x);
+  // departure: the last workgroup out clears the counters for the next launch
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(&sync[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&sync[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+extern "C" int f16_gemm_pair_tune(const void* A1, const void* W1, float* x, const float* ln_g,
+                                  const float* ln_b, const void* W2, const float* b2, void* C16,
+                                  int M, int K, int N1, int N2, unsigned* sync, int fused,
+                                  void* stream) {
+  LLM_REQUIRE(M >= 1 && M <= 16 && K == N1 && K % 32 == 0 && N1 % 16 == 0 && N2 % 32 == 0 &&
+                  ln_fusable(LLM_F16, M, K) && N2 / 16 >= N1 / 16 && N2 / 16 <= 256,
+              "f16_gemm_pair_tune: shape");
+  GemmArgs a1{};
+  a1.a_packed = 1;
+  a1.A = static_cast<const uint8_t*>(A1);
+  a1.B = static_cast<const uint8_t*>(W1);
+  a1.M = M; a1.N = N1; a1.K = K; a1.KS = K / 32;
+  a1.C = x; a1.c_cols = N1; a1.c_ld = N1;
+  a1.w_keep = 1;  // as the C2 decoder (its weights fit the Infinity Cache)
+  GemmArgs a2{};
+  a2.a_packed = 1;
+  a2.B = static_cast<const uint8_t*>(W2);
+  a2.M = M; a2.N = N2; a2.K = N1; a2.KS = N1 / 32;
+  a2.bias = b2; a2.act = LLM_ACT_RELU;
+  a2.c16 = static_cast<_Float16*>(C16);
+  a2.c_cols = 0; a2.c_ld = N2;
+  a2.ln_x = x; a2.ln_g = ln_g; a2.ln_b = ln_b; a2.ln_eps = 1e-5f;
+  a2.w_keep = 1;
+  a2.seam = sync;
+  a2.seam_n = N1 / 16;
+  hipStream_t st = as_stream(stream);
+  hipError_t e;
+  if (!fused) {
+    e = launch_gemm<GemmKind::F16>(a1, st);
+    if (e == hipSuccess) e = launch_gemm<GemmKind::F16>(a2, st);
+  } else {
+    const size_t lds = ln_lds_bytes<GemmKind::F16, 1, 1, 8>(N1);
+    hipLaunchKernelGGL(gemm_pair_f16_kernel, dim3(N2 / 16), dim3(512), lds, st, a1, a2, N1 / 16,
+                       sync);
+    e = hipGetLastError();
+  }
+  return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "f16_gemm_pair_tune");
 }
 
 // The FP16 GEMM with a forced form (A in packed-A order when a_packed).
