@@ -24,6 +24,7 @@ import torch  # noqa: E402
 import llm_capi  # noqa: E402
 
 CFGS = {"c3": dict(B=64, H=16, D=128, T=8192, ts=16),
+        "c1": dict(B=1, H=4, D=64, T=128, ts=16),
         "c2": dict(B=16, H=12, D=64, T=2048, ts=16),
         "c5": dict(B=64, H=32, D=128, T=8192, ts=16),
         # C4: 8 sequences x 4 beams; each sequence's first 240 tiles are one
