@@ -185,7 +185,13 @@ def time_attention_plain(dec, cfg, B, T, max_seq, iters=20):
 
 FORM_NAMES = {0: "direct (one split)", 1: "split + pa_merge_kernel",
               2: "split + pa_merge_row_kernel (merge + per-row int8 quantisation)",
-              3: "split with workgroup merge (packed fp16 o_proj input)"}
+              3: "split with workgroup merge"}
+# what the launch writes, by decoder kind (the INT8 o_proj quantises fp32 rows in
+# its prologue; the FP16 one reads packed fp16 rows)
+FORM_OUT = {"INT8Decoder": {0: " (fp32 rows; the o_proj prologue quantises them)",
+                            1: " (fp32 rows; the o_proj prologue quantises them)",
+                            3: " (fp32 rows; the o_proj prologue quantises them)"},
+            "CUDADecoder": {3: " (packed fp16 o_proj input)"}}
 
 
 def cpu_threads():
@@ -404,6 +410,7 @@ def main():
             if ratio else None,
             "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}>"
                       + (" beam-group" if form & 16 else "") + ": " + FORM_NAMES[form & 15]
+                      + FORM_OUT.get(cfg["cls"], {}).get(form & 15, "")
                       + f", {nsplit} splits (the step's own launch, llm_decoder_run_attention)",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
     if "beams" in cfg:  # logical bytes: every beam reads its whole context

@@ -125,6 +125,7 @@ struct llm_decoder {
 
   int layer_pre(int l, hipStream_t st, const struct Rows& R);
   int layer_attn(int l, hipStream_t st, const struct Rows& R, PaPlan* plan = nullptr);
+  bool quant_prologue(const struct Rows& R) const;
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -410,6 +411,16 @@ int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamm
   return LLM_OK;
 }
 
+// INT8 decode rows whose o_proj can quantise its own input (gemm.hip
+// quant_prologue_ok): the attention writes fp32 rows, merging its splits in
+// the workgroup, and the o_proj prologue quantises them per row -- no merge
+// launch.  Beam groups keep the merge launch (the beam kernel's workgroups
+// are 4 beams of one split), as do prefill chunks.
+bool llm_decoder::quant_prologue(const Rows& R) const {
+  return wdtype == LLM_I8 && R.prefill_row < 0 && R.row_group == 1 &&
+         quant_prologue_ok(R.n, hid, hid);
+}
+
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
@@ -435,7 +446,9 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
   PaRowOutputs ro;
   ro.pack = 1;
   ro.keep_out = 0;
-  if (wdtype == LLM_I8) {
+  if (quant_prologue(R)) {
+    ro.f32_rows = 1;  // fp32 rows in R.o, quantised by the o_proj prologue
+  } else if (wdtype == LLM_I8) {
     ro.q = static_cast<int8_t*>(R.act);
     ro.inv_scale = R.sa;
   } else {
@@ -455,11 +468,19 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.w_keep = w_keep;
   g.A = R.act;
   g.M = R.n;
-  // o_proj: input produced (packed) by the attention merge
-  RET_IF(tap(l, 1, R, hid, st));
+  // o_proj: input produced (packed) by the attention merge, or quantised from
+  // the attention's fp32 rows by the GEMM's own prologue
   g.W_packed = wo.p + sz_o * l; g.N = hid; g.K = hid; g.C = R.x;
   if (i8) { g.sa = R.sa; g.sw = sw_o.p + lh; }
+  const bool qpro = quant_prologue(R);
+  if (qpro) {
+    g.ln_x = R.o;
+    g.ln_quant_only = 1;
+    if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
+  }
   RET_IF(weight_gemm(g, st));
+  g.ln_x = nullptr; g.ln_quant_only = 0; g.act_out = nullptr; g.sa_out = nullptr;
+  RET_IF(tap(l, 1, R, hid, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
   RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;

@@ -162,9 +162,12 @@ __device__ __forceinline__ void ln_prologue(const GemmArgs& a, int m0, uint8_t* 
   const int K = a.K;
   const int K4 = K >> 2;
   const int stride = ln_row_stride(K, ESIZE);
+  // ln_g == NULL: quantise only (I8: the fp32 rows are the attention output,
+  // the o_proj prologue replacing the merge launch's per-row quantisation)
+  const bool do_ln = a.ln_g != nullptr;
   LnRow<CPL> gm, bt;
-  ln_wave_load(a.ln_g, K4, true, gm);
-  ln_wave_load(a.ln_b, K4, true, bt);
+  ln_wave_load(a.ln_g, K4, do_ln, gm);
+  ln_wave_load(a.ln_b, K4, do_ln, bt);
   for (int r0 = w; r0 < ROWS; r0 += 2 * WAVES) {
     LnRow<CPL> x[2];
 #pragma unroll
@@ -183,7 +186,17 @@ __device__ __forceinline__ void ln_prologue(const GemmArgs& a, int m0, uint8_t* 
       const int r = r0 + q * WAVES;
       if (r >= ROWS) break;
       const bool mok = m0 + r < a.M;  // rows past M: zero A (their outputs are not stored)
-      const float am = ln_wave_compute(x[q], gm, bt, K, a.ln_eps);
+      float am;
+      if (do_ln) {
+        am = ln_wave_compute(x[q], gm, bt, K, a.ln_eps);
+      } else {
+        am = 0.f;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(x[q].v[j][e]));
+        am = ln_wave_max(am);
+      }
       uint8_t* rowp = alds + (size_t)r * stride;
       if constexpr (KIND == GemmKind::I8) {
         const float scale = 127.f / (am + 1e-6f);
@@ -649,7 +662,7 @@ struct TileChoice {
   int nt, waves, mrows;
 };
 inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
-  if (a.ln_x || a.partial || a.M <= 16 || a.M > 64) return false;
+  if ((a.ln_x && a.ln_g) || a.partial || a.M <= 16 || a.M > 64) return false;
   if (a.M > 32) {
     if ((a.N + 15) / 16 >= 256) return false;
     t = TileChoice{2, 8, 16};
@@ -794,11 +807,29 @@ bool llm::ln_fusable(int dtype, int M, int K) {
   return (size_t)rows * (ln_row_stride(K, es) + 4) <= kLnLdsMax;
 }
 
+// The quantising prologue (I8 o_proj reading the attention's fp32 rows): the
+// workgroup's rows as the launch will tile them -- 16 at <= 16 rows and in
+// the 16-row forms of 17..64 rows (narrow_decode_tile) -- at most 128 KB of
+// fp32 read per workgroup and an int8 image that fits LDS.
+bool llm::quant_prologue_ok(int M, int N, int K) {
+  if (M <= 0 || M > 64 || K % 256 != 0 || K > 2048 || N % 16 != 0) return false;
+  GemmArgs probe{};
+  probe.M = M; probe.N = N; probe.K = K; probe.KS = K / 64;
+  probe.ln_x = reinterpret_cast<const float*>(16);  // (a quantising prologue: ln_g NULL)
+  TileChoice t{0, 0, 0};
+  const int rows = M <= 16 ? 16 : narrow_decode_tile(probe, 64, t) ? t.mrows : 0;
+  if (rows != 16) return false;
+  return (size_t)rows * K * sizeof(float) <= 128 * 1024 &&
+         (size_t)rows * (ln_row_stride(K, 1) + 4) <= kLnLdsMax;
+}
+
 int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   LLM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0 && (g.A || g.ln_x) && g.W_packed,
               "weight_gemm: bad arguments");
-  LLM_REQUIRE(!g.ln_x || (g.ln_g && g.ln_b && ln_fusable(g.dtype, g.M, g.K)),
-              "weight_gemm: LayerNorm prologue needs gamma / beta and an A image that fits LDS");
+  LLM_REQUIRE(!g.ln_x || (g.ln_quant_only ? g.dtype == LLM_I8 && quant_prologue_ok(g.M, g.N, g.K)
+                                           : g.ln_g && g.ln_b && ln_fusable(g.dtype, g.M, g.K)),
+              "weight_gemm: LayerNorm / quantising prologue needs gamma / beta (LN) and an A "
+              "image that fits LDS");
   const int kstep = g.dtype == LLM_I8 ? 64 : 32;
   LLM_REQUIRE(g.K % kstep == 0 && g.N % 16 == 0, "weight_gemm: K / N alignment");
   LLM_REQUIRE(g.a_packed || (g.lda >= g.K && g.lda % 16 == 0), "weight_gemm: lda");
@@ -814,7 +845,9 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.c_ld = g.c_ld > 0 ? g.c_ld : g.N;
   LLM_REQUIRE(!g.C16 || g.N % 32 == 0, "weight_gemm: packed fp16 output needs N % 32 == 0");
   a.c16 = static_cast<_Float16*>(g.C16);
-  a.ln_x = g.ln_x; a.ln_g = g.ln_g; a.ln_b = g.ln_b; a.ln_eps = g.ln_eps;
+  a.ln_x = g.ln_x; a.ln_eps = g.ln_eps;
+  a.ln_g = g.ln_quant_only ? nullptr : g.ln_g;
+  a.ln_b = g.ln_quant_only ? nullptr : g.ln_b;
   a.ln_emb = g.ln_emb; a.ln_tok = g.ln_tok; a.ln_V = g.ln_V;
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;

@@ -55,6 +55,10 @@ struct WeightGemm {
   void* act_out = nullptr;
   float* sa_out = nullptr;
   int w_keep = 0;  // weights with the default cache policy (kept in the Infinity Cache), else nt
+  // I8: ln_x holds fp32 rows to quantise per row into A (no LayerNorm; ln_g /
+  // ln_b unused) -- the o_proj prologue replacing the attention merge's
+  // quantisation (quant_prologue_ok)
+  int ln_quant_only = 0;
 };
 
 // Input of a LayerNorm when it is not x: embedding rows E[tok[r]] (the decode
@@ -69,5 +73,8 @@ int weight_gemm(const WeightGemm& g, hipStream_t st);
 // Whether weight_gemm can run the LayerNorm prologue for M rows of K (the
 // per-workgroup A image must fit in LDS; K <= 128 groups of 16 bytes).
 bool ln_fusable(int dtype, int M, int K);
+// Whether weight_gemm can run the quantising prologue (ln_quant_only) for an
+// I8 GEMM of M rows, N columns, K inputs.
+bool quant_prologue_ok(int M, int N, int K);
 
 }  // namespace llm

@@ -1949,12 +1949,22 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // fp16 o_proj input only (the FP16 decoder's attention): with at most one
   // merge batch of splits per (b, h) the splits merge inside the split
   // launch's workgroup (C2: 12 merge launches per step fewer), with long splits
-  const bool wgm_ok = row_out && rows->out16 && !rows->q && row_group == 1 &&
+  // fp32 rows for a quantising consumer (the INT8 decoder's o_proj prologue)
+  // merge in the workgroup too, with a split count that divides the CU's 8
+  // resident waves (2 / 4 / 8 waves per workgroup: a 6-wave workgroup would
+  // leave 2 of the 8 slots idle): C3 6 -> 8 splits
+  const bool f32_rows = rows && rows->f32_rows && !rows->q && !rows->out16;
+  const bool wgm_ok = ((row_out && rows->out16 && !rows->q) || f32_rows) && row_group == 1 &&
                       kv->kv_dtype == LLM_F16 && wg_merge_on();
   int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident_launch);
-  if (wgm_ok && pps_fixed <= 0) {
+  if (wgm_ok && pps_fixed <= 0 && !f32_rows) {
     const int nw = choose_nsplit(B, H, ntiles_max, 0, resident_launch, kWgmShortPps);
     if (nw >= 2 && nw <= kWgmMaxSplits) nsplit = nw;
+  }
+  if (wgm_ok && pps_fixed <= 0 && f32_rows && nsplit >= 2) {
+    int nw = 2;
+    while (nw < nsplit && nw < kWgmMaxSplits) nw *= 2;
+    if (nw >= nsplit && (long long)nw * kMaxPps >= ntiles_max) nsplit = nw;
   }
 #if LLM_TUNING
   // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
@@ -2023,7 +2033,8 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   a.nsplit = nsplit;
   a.group = std::max(1, std::min(row_group, 4));
   a.qscale = sm_scale * kLog2e;
-  if (!direct) {
+  const bool wgm = wgm_ok && !direct && a.group == 1 && nsplit <= kWgmMaxSplits;
+  if (!direct && !wgm) {  // (the workgroup merge keeps its splits' states in LDS)
     const size_t need = (size_t)B * H * nsplit * (size_t)(D + 2) * sizeof(float);
     LLM_REQUIRE(workspace != nullptr && workspace_bytes >= need,
                 "pa_decode: workspace too small (see pa_decode_workspace_bytes)");
@@ -2032,12 +2043,11 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   a.balance16 = beam_balance16();
   a.beam4 = use_beam4 ? 1 : 0;
-  const bool wgm = wgm_ok && !direct && a.group == 1 && nsplit <= kWgmMaxSplits;
   if (wgm) {
     a.wgm = 1;
     a.out16 = static_cast<_Float16*>(rows->out16);
     a.pack = rows->pack;
-    a.out = rows->keep_out ? out : nullptr;
+    a.out = rows->keep_out || f32_rows ? out : nullptr;
   }
   hipError_t e;
   bool beam = false;  // the beam kernel ran: every split holds a partial

@@ -17,6 +17,10 @@ struct PaRowOutputs {
   void* out16 = nullptr;
   int pack = 0;  // q / out16 in packed-A order (common.hpp a_frag_off_*)
   int keep_out = 1;  // 0: a split launch skips the fp32 `out` rows (only q / out16 are read)
+  // 1 (with q and out16 NULL): the consumer quantises the fp32 `out` rows
+  // itself (the INT8 o_proj's quantising prologue), so a split launch may
+  // merge its splits inside the workgroup and write `out` (no merge launch)
+  int f32_rows = 0;
 };
 
 // The launch a call takes (pa_decode_plan): splits per (row, head) and

@@ -2,10 +2,11 @@
 the BASELINE configs run.
 
 Inside a decode step the paged attention runs split-T: many splits per (row,
-head), merged by pa_merge_row_kernel, which also quantises each row (all
-heads) into the packed int8 o_proj input (INT8Decoder), or merged inside the
-split workgroup into the packed fp16 o_proj input (CUDADecoder, workgroup
-merge).  That merge is the reference's AV-and-store
+head).  INT8Decoder: up to 8 splits merge inside the split workgroup and more
+in the fp32 merge launch, and the o_proj GEMM's prologue quantises each row
+(all heads) into its int8 A; beam groups (C4) merge in pa_merge_row_kernel,
+which quantises the rows itself.  CUDADecoder: merged inside the split
+workgroup into the packed fp16 o_proj input (workgroup merge).  That merge is the reference's AV-and-store
 (attention_cpu/cpu_attention_kernel.cpp:103-120) followed by the quantiser
 (attention_cpu/int8_quant.cpp:5-13,59-64).
 
@@ -129,18 +130,18 @@ def _int8_decoder(oracle, L, H, D, V, max_seq, rows, seed):
     return w, dec
 
 
-@pytest.mark.parametrize("rows,T", [(4, 2048), (8, 8192)])
-def test_int8_step_multi_split_attention_vs_oracle(gpu, oracle, rows, T):
+@pytest.mark.parametrize("rows,T,form", [(4, 2048, FORM_WG_MERGE), (8, 8192, FORM_SPLIT_MERGE)])
+def test_int8_step_multi_split_attention_vs_oracle(gpu, oracle, rows, T, form):
     """C3 model dims (16 heads x 128), 2 layers, 4 rows at T 2048 and 8 rows at
-    T 8192: the step's attention runs >= 8 splits (16 at T 8192: past the
-    merge kernel's first batch of 8), merged and quantised per row by
-    pa_merge_row_kernel."""
+    T 8192: the step's attention runs >= 8 splits, merged inside the split
+    workgroup (8 splits at T 2048) or by the fp32 merge launch (16 at T 8192),
+    and the o_proj prologue quantises the fp32 rows (the tapped stage-1 A)."""
     from oracle.oracle import OracleDecoder
     w, dec = _int8_decoder(oracle, 2, 16, 128, 512, T + 8, rows, seed=51)
     taps = _Taps(dec, w["cfg"], rows)
     dec.begin_synthetic(rows, T, 77, True)
-    ns, form = dec.attention_plan()
-    assert form == FORM_SPLIT_MERGE_ROW and ns >= 8, (ns, form)
+    ns, got = dec.attention_plan()
+    assert got == form and ns >= 8, (ns, got)
     odec = OracleDecoder(oracle, w, rows)
     decoder_kv_to_oracle(dec, odec, rows, T)
     flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=T)
