@@ -447,7 +447,11 @@ int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* stream);
 int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev);
 /* The attention launch of the decoder's step at its current batch and row
  * group (pa_decode_plan of layer 0's view, T = max_seq_len: the step graph's
- * launch, whose split lengths follow each row's live context). */
+ * launch, whose split lengths follow each row's live context).  INT8 decoders
+ * whose o_proj quantises its own input (decode rows <= 64, hidden <= 2048, no
+ * beam groups) report the fp32-row forms (LLM_PA_FORM_WG_MERGE up to 8
+ * splits, else LLM_PA_FORM_SPLIT_MERGE, LLM_PA_FORM_DIRECT); beam groups and
+ * wider models LLM_PA_FORM_SPLIT_MERGE_ROW (| LLM_PA_FORM_BEAM). */
 int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form);
 /* Enqueue layer `layer`'s attention launch of the decoder's step on `stream`
  * (NULL: the decoder's) -- the same kernels, grid and outputs as inside the
