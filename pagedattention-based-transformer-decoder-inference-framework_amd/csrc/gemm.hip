@@ -661,15 +661,16 @@ inline int pick_waves(const GemmArgs&, int) { return 8; }
 struct TileChoice {
   int nt, waves, mrows;
 };
-inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
-  if ((a.ln_x && a.ln_g) || a.partial || a.M <= 16 || a.M > 64) return false;
-  if (a.M > 32) {
-    if ((a.N + 15) / 16 >= 256) return false;
+// By shape: M rows, N columns, K inputs (the LayerNorm-prologue and split-K
+// launches keep their own forms).
+inline bool narrow_tile_for(int M, int N, int K, TileChoice& t) {
+  if (M <= 16 || M > 64) return false;
+  const int ntiles = (N + 15) / 16;
+  if (M > 32) {
+    if (ntiles >= 256) return false;
     t = TileChoice{2, 8, 16};
     return true;
   }
-  const int ntiles = (a.N + 15) / 16;
-  const int K = a.KS * kstep;
   if (ntiles < 384) {
     t = K >= 4096 ? TileChoice{1, 8, 16} : TileChoice{1, 4, 16};
     return true;
@@ -679,6 +680,10 @@ inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
     return true;
   }
   return false;
+}
+inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
+  if ((a.ln_x && a.ln_g) || a.partial) return false;
+  return narrow_tile_for(a.M, a.N, a.KS * kstep, t);
 }
 
 template <GemmKind KIND>
@@ -813,11 +818,8 @@ bool llm::ln_fusable(int dtype, int M, int K) {
 // fp32 read per workgroup and an int8 image that fits LDS.
 bool llm::quant_prologue_ok(int M, int N, int K) {
   if (M <= 0 || M > 64 || K % 256 != 0 || K > 2048 || N % 16 != 0) return false;
-  GemmArgs probe{};
-  probe.M = M; probe.N = N; probe.K = K; probe.KS = K / 64;
-  probe.ln_x = reinterpret_cast<const float*>(16);  // (a quantising prologue: ln_g NULL)
   TileChoice t{0, 0, 0};
-  const int rows = M <= 16 ? 16 : narrow_decode_tile(probe, 64, t) ? t.mrows : 0;
+  const int rows = M <= 16 ? 16 : narrow_tile_for(M, N, K, t) ? t.mrows : 0;
   if (rows != 16) return false;
   return (size_t)rows * K * sizeof(float) <= 128 * 1024 &&
          (size_t)rows * (ln_row_stride(K, 1) + 4) <= kLnLdsMax;
