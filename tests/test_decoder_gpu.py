@@ -682,13 +682,15 @@ def test_forced_step_48_rows(gpu, oracle):
     assert n_flips < 1e-3 * n_vals
 
 
-@pytest.mark.parametrize("rows", [24, 48])
+@pytest.mark.parametrize("rows", [24, 40, 48])
 def test_forced_hidden_2048_tile_forms(gpu, oracle, rows):
     """hid 2048: the LayerNorms are launches (the rows' fp32 image is too big
-    for the GEMM prologue).  At 48 rows o_proj and fc2 run 2-column-tile
-    16-row workgroups (three row blocks; round 2 ran split-K here); at 24 rows
-    the GEMMs take the narrow 16-row tiles (two row blocks, 4-wave workgroups
-    for K < 4096).  Teacher forced, north_star bar."""
+    for the GEMM prologue).  At 40 / 48 rows o_proj and fc2 run 2-column-tile
+    16-row workgroups (three row blocks, the last one partial at 40; round 2
+    ran split-K here); at 24 rows the GEMMs take the narrow 16-row tiles (two
+    row blocks, 4-wave workgroups for K < 4096).  o_proj quantises the
+    attention's fp32 rows in its prologue at every one of these row counts
+    (the tapped stage-1 A).  Teacher forced, north_star bar."""
     from oracle.oracle import OracleDecoder
     w = _int8_model(oracle, L=2, H=16, D=128, V=512, S=24, seed=41)
     dec = _make_gpu_decoder(w, max_batch=rows)
