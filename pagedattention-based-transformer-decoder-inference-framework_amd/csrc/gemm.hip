@@ -89,6 +89,7 @@ struct GemmArgs {
   // LayerNorm-prologue tile waits on after issuing its first weight batches
   unsigned* seam;
   int seam_n;
+  int qdiag;  // tuning build, timing only: bit0 skip the prologue, bit1 no weight loads before it
 };
 
 // LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
@@ -409,12 +410,19 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int
   bool b1_pre = false;  // b1's weight loads already issued
   if constexpr (PRO != 0) {
     // the first two batches' weights are in flight while the prologue runs
-    if (ks0 < ks1) issue(b0, ks0, false, true);
-    if (ks0 + kUnroll < ks1) {
+    bool pre = true;
+#if LLM_TUNING
+    pre = (a.qdiag & 2) == 0;
+#endif
+    if (pre && ks0 < ks1) issue(b0, ks0, false, true);
+    if (pre && ks0 + kUnroll < ks1) {
       issue(b1, ks0 + kUnroll, false, true);
       b1_pre = true;
     }
     if constexpr (SEAM != 0) seam_wait(a.seam, a.seam_n);  // weights already in flight
+#if LLM_TUNING
+    if ((a.qdiag & 1) == 0)
+#endif
     ln_prologue<KIND, ROWS_, WAVES>(a, m0, alds, sa_lds);
     __syncthreads();
     if constexpr (KIND == GemmKind::I8) {
@@ -441,7 +449,11 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int
 
   {
     int ks = ks0;
-    if (ks < ks1) issue(b0, ks, true, PRO == 0);
+    bool b0_b = PRO == 0;
+#if LLM_TUNING
+    if constexpr (PRO != 0) b0_b = (a.qdiag & 2) != 0;  // weights not issued before the prologue
+#endif
+    if (ks < ks1) issue(b0, ks, true, b0_b);
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const int o = threadIdx.x + e * NTHR;
@@ -932,6 +944,24 @@ extern "C" int i8_gemm_tune(int nt, int waves, int mrows, int a_packed, const in
   a.sa = sa; a.sw = sw; a.C = C; a.c_cols = N; a.c_ld = N;
   hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream), nt, waves, mrows);
   return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune");
+}
+
+// The quantising prologue as the decoder's o_proj runs it (weight_gemm with
+// ln_quant_only): fp32 rows x [M][K] quantised per row in the prologue, the
+// product-path tile choice; for timing against i8_gemm_tune on packed int8 A.
+extern "C" int i8_gemm_tune_qpro(const float* x, const void* W_packed, float* C, int M, int N,
+                                 int K, const float* sw, int qdiag, void* stream) {
+  LLM_REQUIRE(quant_prologue_ok(M, N, K), "i8_gemm_tune_qpro: shape");
+  GemmArgs a{};
+  a.a_packed = 1;
+  a.B = static_cast<const uint8_t*>(W_packed);
+  a.M = M; a.N = N; a.K = K; a.KS = K / 64;
+  a.sw = sw; a.C = C; a.c_cols = N; a.c_ld = N;
+  a.ln_x = x;  // ln_g NULL: the quantising prologue
+  a.ln_eps = 1e-5f;
+  a.qdiag = qdiag;
+  hipError_t e = launch_gemm<GemmKind::I8>(a, as_stream(stream));
+  return e == hipSuccess ? LLM_OK : fail(LLM_ERR_HIP, "i8_gemm_tune_qpro");
 }
 
 // Split-K forms: int32 partial slices only (acc_out [kslices][M][N]), packed A;
