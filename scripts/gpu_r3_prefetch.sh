@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3): LLM_PREFETCH and its prefetch_lines_kernel graph branch existed only
+# for this A/B and were removed after it (profiles/r03/prefetch_branch_ab.txt).
 # Weight-prefetch side branch: bench arms per config, then a kernel trace of
 # the best arm (per-GEMM times with prefetched weights).
 set -o pipefail

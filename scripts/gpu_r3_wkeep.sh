@@ -1,4 +1,7 @@
 #!/bin/bash
+# HISTORICAL (round 3): the LLM_WKEEP / LLM_LMKEEP / LLM_DIAG_SKIP_FC1_QUANT switches existed
+# only for this A/B and were removed after it; the winning policy is decoder.cpp w_keep_for
+# (profiles/r03/wkeep_ab.txt).
 # GEMM weight cache policy A/B (default policy = kept in the Infinity Cache vs nt).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
