@@ -233,6 +233,116 @@ __global__ __launch_bounds__(WAVES * 64) void lm_head_kernel(LmHeadArgs a) {
   }
 }
 
+// <= 16 rows with K <= 2048: x is staged into LDS ONCE for the whole K (hi / lo
+// fragments, KS x 2 KiB of dynamic LDS) behind one barrier; then every wave
+// streams its vocabulary tile's E with two 8-k-step batches in flight and no
+// further barrier (lm_head_kernel stages x per 256-wide chunk, two barriers
+// each, so every chunk waits for the workgroup's slowest E load).  Same
+// MFMA sequence per tile (hi then lo, k ascending): the same logits bit for
+// bit as lm_head_kernel<1, 16, 1>.
+__global__ __launch_bounds__(1024) void lm_head_x1_kernel(LmHeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 xs[];  // [KS][hi/lo][64 lanes]
+  __shared__ float pv[kLmWaves][16];
+  __shared__ int pi[kLmWaves][16];
+  const int lane = lane_id();
+  const int w = wave_id_uniform();
+  const int m0 = blockIdx.y * 16;
+  const int KS = a.K / 32;
+  const int ntiles = (a.V + 15) / 16;
+  const auto ers = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.E, (short)0, (uint32_t)min((size_t)ntiles * KS * 1024, (size_t)0xFFFFFFF0u), 0x00020000);
+  const int ntile = blockIdx.x * a.tiles + w;
+  const bool mine = w < a.tiles;  // a wave past `tiles` only stages x
+  const uint32_t e_off =
+      mine && ntile < ntiles ? (uint32_t)((size_t)ntile * KS * 1024) + lane * 16 : 0xFFFFFFF0u;
+  constexpr int U = 8;
+  u32x4 eA[U], eB[U];
+  auto issue = [&](u32x4 (&d)[U], int k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u;
+      const uint32_t off = (e_off == 0xFFFFFFF0u || k >= KS) ? 0xFFFFFFF0u : e_off + (uint32_t)k * 1024u;
+      d[u] = __builtin_amdgcn_raw_buffer_load_b128(ers, off, 0, 2);  // E: read once, nt
+    }
+  };
+  if (mine) issue(eA, 0);  // the first E batch is in flight while x is staged
+  // x fragment (ks, lane l): row m0 + (l & 15), k = 32 ks + 8 (l >> 4) .. +8
+  for (int f = threadIdx.x; f < KS * 64; f += 1024) {
+    const int l = f & 63, ks = f >> 6;
+    const int row = m0 + (l & 15);
+    const int k = ks * 32 + 8 * (l >> 4);
+    f32x4 x0{0.f, 0.f, 0.f, 0.f}, x1{0.f, 0.f, 0.f, 0.f};
+    if (row < a.M) {
+      const f32x4* src = reinterpret_cast<const f32x4*>(a.x + (size_t)row * a.K + k);
+      x0 = src[0];
+      x1 = src[1];
+    }
+    f16x8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      hi[e] = (_Float16)x0[e];
+      hi[4 + e] = (_Float16)x1[e];
+      lo[e] = (_Float16)(x0[e] - (float)hi[e]);
+      lo[4 + e] = (_Float16)(x1[e] - (float)hi[4 + e]);
+    }
+    xs[(ks * 2) * 64 + l] = __builtin_bit_cast(u32x4, hi);
+    xs[(ks * 2 + 1) * 64 + l] = __builtin_bit_cast(u32x4, lo);
+  }
+  __syncthreads();
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const u32x4 (&d)[U], int k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u;
+      if (k >= KS) break;
+      const f16x8 bb = __builtin_bit_cast(f16x8, d[u]);
+      const f16x8 hi = __builtin_bit_cast(f16x8, xs[(k * 2) * 64 + lane]);
+      const f16x8 lo = __builtin_bit_cast(f16x8, xs[(k * 2 + 1) * 64 + lane]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bb, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bb, acc, 0, 0, 0);
+    }
+  };
+  if (mine) {
+    for (int k0 = 0; k0 < KS; k0 += 2 * U) {
+      if (k0 + U < KS) issue(eB, k0 + U);
+      mm(eA, k0);
+      if (k0 + U >= KS) break;
+      if (k0 + 2 * U < KS) issue(eA, k0 + 2 * U);
+      mm(eB, k0 + U);
+    }
+  }
+  // acc lane l, reg r: x row m0 + 4 (l >> 4) + r, vocabulary row 16 ntile + (l & 15)
+  const int n = mine ? ntile * 16 + (lane & 15) : a.V;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * (lane >> 4) + r;
+    const float v = acc[r];
+    if (a.logits && m0 + row < a.M && n < a.V) a.logits[(size_t)(m0 + row) * a.V + n] = v;
+    if (a.part_val) {
+      float bv = n < a.V ? v : -INFINITY;
+      int bi = n < a.V ? n : 0x7fffffff;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if ((lane & 15) == 0) { pv[w][row] = bv; pi[w][row] = bi; }
+    }
+  }
+  if (!a.part_val) return;
+  __syncthreads();
+  if (threadIdx.x < 16 && m0 + (int)threadIdx.x < a.M) {
+    const int row = threadIdx.x;
+    float bv = pv[0][row];
+    int bi = pi[0][row];
+    for (int ww = 1; ww < a.tiles; ++ww)  // tiles in increasing vocabulary order
+      if (pv[ww][row] > bv) { bv = pv[ww][row]; bi = pi[ww][row]; }
+    a.part_val[(size_t)(m0 + row) * a.nwg + blockIdx.x] = bv;
+    a.part_idx[(size_t)(m0 + row) * a.nwg + blockIdx.x] = bi;
+  }
+}
+
 // Per row: the first maximum over the workgroup partials (in vocabulary order).
 // pos / ctx (optional): the decode step's position advance of the row, fused
 // here instead of a launch of its own.
@@ -359,7 +469,10 @@ hipError_t launch_lm_head(const float* x, const void* E, float* logits, int M, i
     return hipGetLastError();
   }
 #endif
-  if (mt == 1) hipLaunchKernelGGL((lm_head_kernel<1, 16, 1>), grid, dim3(1024), 0, st, a);
+  if (mt == 1 && a.K <= 2048 && mode == 0) {
+    const size_t lds = (size_t)(a.K / 32) * 2 * 64 * sizeof(u32x4);
+    hipLaunchKernelGGL(lm_head_x1_kernel, grid, dim3(1024), lds, st, a);
+  } else if (mt == 1) hipLaunchKernelGGL((lm_head_kernel<1, 16, 1>), grid, dim3(1024), 0, st, a);
   else if (mt == 2) hipLaunchKernelGGL((lm_head_kernel<2, 16, 1>), grid, dim3(1024), 0, st, a);
   else hipLaunchKernelGGL((lm_head_kernel<4, 16, 1>), grid, dim3(1024), 0, st, a);
   return hipGetLastError();
