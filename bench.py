@@ -192,6 +192,8 @@ FORM_OUT = {"INT8Decoder": {0: " (fp32 rows; the o_proj prologue quantises them)
                             1: " (fp32 rows; the o_proj prologue quantises them)",
                             3: " (fp32 rows; the o_proj prologue quantises them)"},
             "CUDADecoder": {3: " (packed fp16 o_proj input)"}}
+# form bit 32: the FP16 decoder's o_proj runs inside the workgroup merge
+OPROJ_OUT = " (o_proj fused: each (row, head) workgroup adds o_h W_o[h] into int64 rows)"
 
 
 def cpu_threads():
@@ -410,7 +412,7 @@ def main():
             if ratio else None,
             "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}>"
                       + (" beam-group" if form & 16 else "") + ": " + FORM_NAMES[form & 15]
-                      + FORM_OUT.get(cfg["cls"], {}).get(form & 15, "")
+                      + (OPROJ_OUT if form & 32 else FORM_OUT.get(cfg["cls"], {}).get(form & 15, ""))
                       + f", {nsplit} splits (the step's own launch, llm_decoder_run_attention)",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
     if "beams" in cfg:  # logical bytes: every beam reads its whole context

@@ -91,6 +91,7 @@ int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles)
 #define LLM_PA_FORM_SPLIT_MERGE_ROW 2 /* split launch + pa_merge_row_kernel (o_proj input) */
 #define LLM_PA_FORM_WG_MERGE 3        /* splits merged inside the split workgroup */
 #define LLM_PA_FORM_BEAM 16
+#define LLM_PA_FORM_OPROJ 32 /* FP16 decoder: o_proj fused into the workgroup merge */
 int pa_decode_plan(const pa_kv_view* kv, int B, int H, int D, int T, int pages_per_split,
                    int row_group, int* nsplit, int* form);
 
@@ -451,7 +452,9 @@ int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev);
  * whose o_proj quantises its own input (decode rows <= 64, hidden <= 2048, no
  * beam groups) report the fp32-row forms (LLM_PA_FORM_WG_MERGE up to 8
  * splits, else LLM_PA_FORM_SPLIT_MERGE, LLM_PA_FORM_DIRECT); beam groups and
- * wider models LLM_PA_FORM_SPLIT_MERGE_ROW (| LLM_PA_FORM_BEAM). */
+ * wider models LLM_PA_FORM_SPLIT_MERGE_ROW (| LLM_PA_FORM_BEAM).  FP16
+ * decoders whose launch merges in the workgroup (2..8 splits, head_dim <= 128,
+ * <= 64 heads) run o_proj inside it: LLM_PA_FORM_WG_MERGE | LLM_PA_FORM_OPROJ. */
 int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form);
 /* Enqueue layer `layer`'s attention launch of the decoder's step on `stream`
  * (NULL: the decoder's) -- the same kernels, grid and outputs as inside the

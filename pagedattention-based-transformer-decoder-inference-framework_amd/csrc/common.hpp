@@ -49,6 +49,28 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 constexpr float kNegSentinel = -1.0e30f;  // "minus infinity" that stays finite
 constexpr float kLog2e = 1.4426950408889634f;
 
+// Counted fixed-point accumulator of the FP16 decoder's fused o_proj
+// (pa_decode.hip, workgroup merge): the H (row, head) workgroups of a row each
+// add their head's product o_h . W_o[h] into one int64 per output column as
+// 2^56 (an arrival count in the top bits) + the product in units of 2^-32.
+// Integer addition is order-independent, so the sum is the same bits whatever
+// order the heads' atomics land in (fp32 atomics would not be), and the adder
+// whose returned old value counts H - 1 arrivals holds the complete sum: it
+// stores the fp32 value and clears the column for the next layer.  Exact to
+// 2^-33 per head for |sum| < 2^23 (8.4e6) and H <= 64.
+constexpr float kOAccScale = 4294967296.f;  // 2^32
+constexpr long long kOAccCount = 1LL << 56;
+__device__ __forceinline__ long long oacc_term(float v) {
+  return __float2ll_rn(v * kOAccScale) + kOAccCount;
+}
+__device__ __forceinline__ int oacc_count(long long v) {
+  return (int)((v + (kOAccCount >> 1)) >> 56);
+}
+__device__ __forceinline__ float oacc_value(long long v) {
+  const long long f = v - (long long)oacc_count(v) * kOAccCount;
+  return (float)((double)f * (1.0 / 4294967296.0));
+}
+
 // DPP lane moves (row = 16 lanes).  ctrl must be a compile-time constant.
 template <int CTRL>
 __device__ __forceinline__ float mov_dpp(float x) {

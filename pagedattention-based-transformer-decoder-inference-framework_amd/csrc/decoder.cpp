@@ -73,6 +73,9 @@ struct llm_decoder {
   DevBuf<uint8_t> emb_packed;  // LM-head copy of emb in B-fragment order
   DevBuf<float> ln1_g, ln1_b, ln2_g, ln2_b, b1, b2, sw_qkv, sw_o, sw1, sw2;
   DevBuf<uint8_t> wqkv, wo, w1, w2;  // packed, L consecutive blocks
+  // FP16: W_o again as per-head column slices for the fused o_proj,
+  // [L][H][D/8][hid][8] (PaRowOutputs::wo_heads)
+  DevBuf<uint16_t> wo_heads;
   size_t sz_qkv = 0, sz_o = 0, sz_1 = 0, sz_2 = 0;
   bool weights_ready = false;
   int w_keep = 0;  // the GEMM weights fit the Infinity Cache: keep them there (w_keep_for)
@@ -87,6 +90,9 @@ struct llm_decoder {
   int lm_nwg = 0;
   DevBuf<int8_t> qa;
   DevBuf<uint16_t> a16;
+  // FP16: the fused o_proj's int64 columns [max_batch][hid] (zero between
+  // attention launches: the adder completing a column clears it)
+  DevBuf<long long> oacc;
   DevBuf<int32_t> tokens, pos, ctx;
   DevBuf<uint8_t> attn_ws;
   size_t attn_ws_bytes = 0;
@@ -126,6 +132,7 @@ struct llm_decoder {
   int layer_pre(int l, hipStream_t st, const struct Rows& R);
   int layer_attn(int l, hipStream_t st, const struct Rows& R, PaPlan* plan = nullptr);
   bool quant_prologue(const struct Rows& R) const;
+  bool oproj_fusable(const struct Rows& R);
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -189,7 +196,11 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->sa.alloc((size_t)B));
   const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
   RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
-  if (d->wdtype == LLM_F16) RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
+  if (d->wdtype == LLM_F16) {
+    RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
+    RET_IF(d->oacc.alloc((size_t)B * hid));
+    LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * B * hid));
+  }
   d->b16 = B16;
   RET_IF(d->tokens.alloc((size_t)B));
   RET_IF(d->pos.alloc((size_t)B));
@@ -312,6 +323,22 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
   RET_IF(upload_common(d, w->emb, w->ln1_g, w->ln1_b, w->ln2_g, w->ln2_b));
   RET_IF(upload_packed(d->wqkv, d->sz_qkv, w->wqkv, L, hid, 3 * hid, LLM_F16, "wqkv"));
   RET_IF(upload_packed(d->wo, d->sz_o, w->wo, L, hid, hid, LLM_F16, "wo"));
+  if (d->D % 8 == 0 && d->D <= 128) {  // the fused o_proj's head slices: [h][kg][n][j] = W_o[h D + 8 kg + j][n]
+    const int D = d->D, KG = D / 8;
+    const uint16_t* src = static_cast<const uint16_t*>(w->wo);
+    std::vector<uint16_t> sl((size_t)hid * hid);
+    RET_IF(d->wo_heads.alloc((size_t)L * hid * hid));
+    for (int l = 0; l < L; ++l) {
+      const uint16_t* wl = src + (size_t)l * hid * hid;
+      for (int h = 0; h < d->H; ++h)
+        for (int kg = 0; kg < KG; ++kg)
+          for (int n = 0; n < hid; ++n)
+            for (int j = 0; j < 8; ++j)
+              sl[(((size_t)h * KG + kg) * hid + n) * 8 + j] = wl[(size_t)(h * D + 8 * kg + j) * hid + n];
+      LLM_HIP_RET(hipMemcpy(d->wo_heads.p + (size_t)l * hid * hid, sl.data(),
+                            sizeof(uint16_t) * hid * hid, hipMemcpyHostToDevice));
+    }
+  }
   RET_IF(upload_packed(d->w1, d->sz_1, w->w1, L, hid, inter, LLM_F16, "w1"));
   RET_IF(upload_packed(d->w2, d->sz_2, w->w2, L, inter, hid, LLM_F16, "w2"));
   RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
@@ -348,6 +375,11 @@ struct Rows {
   int prefill_p0 = 0;
   uint8_t* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
+  // FP16 decode rows: the o_proj runs inside the attention's workgroup merge
+  // (oproj_fusable) through these int64 columns and writes oproj_out (x, or a
+  // scratch row for llm_decoder_run_attention); no o_proj launch
+  long long* oacc = nullptr;
+  float* oproj_out = nullptr;
 };
 
 // Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
@@ -421,6 +453,25 @@ bool llm_decoder::quant_prologue(const Rows& R) const {
          quant_prologue_ok(R.n, hid, hid);
 }
 
+// FP16 decode rows whose o_proj the attention's workgroup merge can run
+// (pa_decode.hip, OPROJ): each (row, head) workgroup multiplies its merged
+// head by W_o's rows for that head and adds the products into the int64
+// columns R.oacc; the adder completing a column writes x (what the o_proj
+// GEMM wrote).  One launch per layer fewer (C2: the 4.9 us o_proj GEMM).
+// Needs the workgroup-merge form (2..8 splits), head_dim <= 128 and <= 64
+// heads; otherwise the o_proj GEMM runs as before.
+bool llm_decoder::oproj_fusable(const Rows& R) {
+  if (wdtype != LLM_F16 || R.prefill_row >= 0 || R.row_group != 1 || R.beam_rows || !wo_heads.p ||
+      D > 128 || H > 64 || !oproj_fuse_on())
+    return false;
+  Rows r = R;
+  r.oacc = oacc.p;
+  r.oproj_out = R.x;
+  PaPlan p;
+  if (layer_attn(0, stream, r, &p) != LLM_OK) return false;
+  return (p.form & LLM_PA_FORM_OPROJ) != 0;
+}
+
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
@@ -451,6 +502,12 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
   } else if (wdtype == LLM_I8) {
     ro.q = static_cast<int8_t*>(R.act);
     ro.inv_scale = R.sa;
+  } else if (R.oacc) {
+    ro.o_acc = R.oacc;
+    ro.o_x = R.oproj_out;
+    ro.wo_heads = wo_heads.p + (size_t)l * hid * hid;
+    ro.o_n = hid;
+    ro.out16 = tap_q ? R.act : nullptr;  // the taps read the packed o_proj input
   } else {
     ro.out16 = R.act;
   }
@@ -478,7 +535,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
     g.ln_quant_only = 1;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
   }
-  RET_IF(weight_gemm(g, st));
+  if (!R.oacc) RET_IF(weight_gemm(g, st));  // (fused: the attention wrote x)
   g.ln_x = nullptr; g.ln_quant_only = 0; g.act_out = nullptr; g.sa_out = nullptr;
   RET_IF(tap(l, 1, R, hid, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
@@ -590,7 +647,8 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
 
 // One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
-  const Rows R = step_rows(0, batch, attn_ws.p);
+  Rows R = step_rows(0, batch, attn_ws.p);
+  if (oproj_fusable(R)) R.oacc = oacc.p, R.oproj_out = R.x;
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -743,6 +801,7 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   d->row_group = 1;
   d->h_pos.assign(d->maxB, 0);
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
+  if (d->oacc.p) LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * d->oacc.n));
   std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
   LLM_HIP_RET(hipMemcpy(d->pos.p, pos.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
   LLM_HIP_RET(hipMemcpy(d->ctx.p, ctx.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
@@ -852,7 +911,8 @@ extern "C" int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form
   LLM_REQUIRE(d && nsplit && form, "llm_decoder_attention_plan: NULL");
   std::lock_guard<std::mutex> g(d->mu);
   LLM_REQUIRE(d->batch > 0, "llm_decoder_attention_plan: no active rows");
-  const Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
+  Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
+  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.x;
   PaPlan p;
   RET_IF(d->layer_attn(0, d->stream, R, &p));
   *nsplit = p.nsplit;
@@ -866,7 +926,10 @@ extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream
   LLM_REQUIRE(d->batch > 0, "llm_decoder_run_attention: no active rows");
   LLM_REQUIRE(layer >= 0 && layer < d->L, "llm_decoder_run_attention: layer out of range");
   hipStream_t st = stream ? as_stream(stream) : d->stream;
-  return d->layer_attn(layer, st, d->step_rows(0, d->batch, d->attn_ws.p));
+  Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
+  // the step's fused o_proj writes the attention rows' fp32 buffer here, not x
+  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.o;
+  return d->layer_attn(layer, st, R);
 }
 
 extern "C" int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,

@@ -77,9 +77,17 @@ struct PaSplitArgs {
   int pack;
   int wgm;
   int beam4;  // row_group 4: pa_beam4_kernel (one wave per (group, head, split))
+  // WGM, fused o_proj (PaRowOutputs::o_acc): o_acc[b][o_n] += o_h . W_o[h rows]
+  // (counted fixed point, common.hpp oacc_term); the last head's adder of a
+  // column stores o_x[b][n] and clears the column
+  long long* o_acc;
+  float* o_x;
+  const _Float16* wo_heads;  // [H][D/8][o_n][8]
+  int o_n;
 };
 
 constexpr int kWgmMaxSplits = 8;  // one merge batch (pa_merge_row_kernel's kMergeBatch)
+constexpr int kOprojMaxD = 128;   // fused o_proj: two W_o column slices of D fp16 in VGPRs
 
 constexpr int kMaxPps = 128;     // page ids held in two registers per lane
 constexpr int kMaxSplits = 128;  // split weights held in two registers per merge lane
@@ -144,9 +152,10 @@ constexpr int kKvLoadAux = 2;
 // of the split (beam-private pages) takes the per-wave direct path.
 // WGM: the workgroup-merge form (PaSplitArgs::wgm): blockDim = 64 * nsplit,
 // one workgroup per (b, h), wave w = split w.
+// OPROJ (WGM only): the fused o_proj of the FP16 decoder (PaSplitArgs::o_acc).
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
-          int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false>
+          int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -161,6 +170,7 @@ void pa_split_kernel(PaSplitArgs a) {
   static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1, "bad D/TS");
 
   static_assert(!(WGM && (DIRECT || BEAM)), "the workgroup merge is a split form");
+  static_assert(!OPROJ || (WGM && KVT == LLM_F16), "the fused o_proj is a workgroup-merge form");
   const int lane = lane_id();
   const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
   const int G = BEAM ? 4 : WGM ? 1 : a.group;
@@ -515,56 +525,125 @@ void pa_split_kernel(PaSplitArgs a) {
       wg_ml[s][0] = m;
       wg_ml[s][1] = l;
     }
+    // OPROJ: wave s takes o_proj columns s*64 + lane + j*64*nsplit, CF columns
+    // per round (CF * D fp16 = 128 VGPRs; each load instruction 1 KiB
+    // contiguous); the first round's W_o slices are in flight across the merge
+    constexpr int KG = D / 8;
+    constexpr int CF = KG >= 32 ? 1 : 32 / KG;
+    const int o_n = OPROJ ? a.o_n : 0;
+    const int ocol0 = s * 64 + lane;
+    const int ostride = 64 * a.nsplit;
+    f16x8 wcur[OPROJ ? CF : 1][OPROJ ? KG : 1];
+    auto load_round = [&](int base) {
+#pragma unroll
+      for (int j = 0; j < CF; ++j) {
+        const f16x8* src = reinterpret_cast<const f16x8*>(a.wo_heads) + (size_t)h * KG * o_n +
+                           min(base + j * ostride, o_n - 1);
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) wcur[j][kg] = src[(size_t)kg * o_n];
+      }
+    };
+    if constexpr (OPROJ) load_round(ocol0);
     __syncthreads();
-    if (s != 0) return;
-    const int pps = row_pps(a.pps, a.nsplit, ntiles);
-    const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
-    const float m0 = lane < ns ? wg_ml[lane][0] : kNegSentinel;
-    const float l0 = lane < ns ? wg_ml[lane][1] : 0.f;
-    const float M = ln_wave_max(fmaxf(m0, kNegSentinel));
-    float o[EPL];
+    if (!OPROJ && s != 0) return;
+    __shared__ __attribute__((aligned(16))) _Float16 wg_o[OPROJ ? D : 8];
+    if (s == 0) {
+      const int pps = row_pps(a.pps, a.nsplit, ntiles);
+      const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
+      const float m0 = lane < ns ? wg_ml[lane][0] : kNegSentinel;
+      const float l0 = lane < ns ? wg_ml[lane][1] : 0.f;
+      const float M = ln_wave_max(fmaxf(m0, kNegSentinel));
+      float o[EPL];
 #pragma unroll
-    for (int e = 0; e < EPL; ++e) o[e] = 0.f;
-    if (ns > 0 && M > 0.5f * kNegSentinel) {
-      const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
-      float L = 0.f;
+      for (int e = 0; e < EPL; ++e) o[e] = 0.f;
+      if (ns > 0 && M > 0.5f * kNegSentinel) {
+        const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
+        float L = 0.f;
 #pragma unroll
-      for (int s2 = 0; s2 < kWgmMaxSplits; ++s2)
-        if (s2 < ns) {
-          const float ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l0), s2));
-          const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
-          L += ls * ws;
+        for (int s2 = 0; s2 < kWgmMaxSplits; ++s2)
+          if (s2 < ns) {
+            const float ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l0), s2));
+            const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
+            L += ls * ws;
+          }
+        const float inv = 1.0f / (L + 1e-6f);
+        float am[EPL];
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) am[e] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < kWgmMaxSplits; ++s2) {
+          const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));  // 0 past ns
+          const float* src = &wg_acc[min(s2, max(ns - 1, 0))][c * EPL];
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) am[e] += src[e] * ws;
         }
-      const float inv = 1.0f / (L + 1e-6f);
-      float am[EPL];
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) am[e] = 0.f;
-#pragma unroll
-      for (int s2 = 0; s2 < kWgmMaxSplits; ++s2) {
-        const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));  // 0 past ns
-        const float* src = &wg_acc[min(s2, max(ns - 1, 0))][c * EPL];
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) am[e] += src[e] * ws;
+        for (int e = 0; e < EPL; ++e) o[e] = am[e] * inv;
       }
+      if (lane < LPT) {
+        const int hid = a.H * D;
+        const int k0 = h * D + c * EPL;
+        if (a.out) {
+          float* op = a.out + (size_t)b * hid + k0;
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) o[e] = am[e] * inv;
-    }
-    if (lane < LPT) {
-      const int hid = a.H * D;
-      const int k0 = h * D + c * EPL;
-      if (a.out) {
-        float* op = a.out + (size_t)b * hid + k0;
+          for (int e = 0; e < EPL; e += 4) *reinterpret_cast<f32x4*>(op + e) = f32x4{o[e], o[e + 1], o[e + 2], o[e + 3]};
+        }
+        if (a.out16) {
+          static_assert(KVT != LLM_F16 || EPL == 8, "fp16 lanes hold 8 dims: one 16-byte store");
+          if constexpr (EPL == 8) {
+            f16x8 pk;
 #pragma unroll
-        for (int e = 0; e < EPL; e += 4) *reinterpret_cast<f32x4*>(op + e) = f32x4{o[e], o[e + 1], o[e + 2], o[e + 3]};
+            for (int e = 0; e < 8; ++e) pk[e] = (_Float16)o[e];
+            *reinterpret_cast<f16x8*>(a.out16 + (a.pack ? a_frag_off_f16(b, k0, hid >> 5)
+                                                        : (size_t)b * hid + k0)) = pk;
+          }
+        }
+        if constexpr (OPROJ) {
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) wg_o[c * EPL + e] = (_Float16)o[e];
+        }
       }
-      if (a.out16) {
-        static_assert(KVT != LLM_F16 || EPL == 8, "fp16 lanes hold 8 dims: one 16-byte store");
-        if constexpr (EPL == 8) {
-          f16x8 pk;
+    }  // s == 0
+    if constexpr (OPROJ) {
+      // o_acc[b][n] += sum_k o16[k] W_o[h D + k][n] for this wave's columns:
+      // fp16 products, fp32 sums (v_dot2_f32_f16), one returning int64 atomic
+      // per column (64 consecutive columns = 512 B per atomic instruction); the
+      // adder that completes a column (H - 1 arrivals before it) stores the
+      // row value x[b][n] and clears the column for the next layer
+      __syncthreads();
+      long long* orow = a.o_acc + (size_t)b * o_n;
+      const f16x2* op = reinterpret_cast<const f16x2*>(wg_o);
+      for (int base = ocol0; base < o_n; base += CF * ostride) {
+        if (base != ocol0) load_round(base);
+        float pj[CF];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) pk[e] = (_Float16)o[e];
-          *reinterpret_cast<f16x8*>(a.out16 + (a.pack ? a_frag_off_f16(b, k0, hid >> 5)
-                                                      : (size_t)b * hid + k0)) = pk;
+        for (int j = 0; j < CF; ++j) {
+          float p = 0.f;
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              p = __builtin_amdgcn_fdot2(f16x2{wcur[j][kg][2 * e], wcur[j][kg][2 * e + 1]},
+                                         op[kg * 4 + e], p, false);
+          pj[j] = p;
+        }
+        // every column's atomic in flight before any result is used
+        long long tj[CF], oj[CF];
+#pragma unroll
+        for (int j = 0; j < CF; ++j) {
+          const int n = base + j * ostride;
+          tj[j] = oacc_term(pj[j]);
+          oj[j] = n < o_n ? (long long)atomicAdd(reinterpret_cast<unsigned long long*>(orow + n),
+                                                 (unsigned long long)tj[j])
+                          : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < CF; ++j) {
+          const int n = base + j * ostride;
+          if (n < o_n && oacc_count(oj[j]) == a.H - 1) {
+            a.o_x[(size_t)b * o_n + n] = oacc_value(oj[j] + tj[j]);
+            __hip_atomic_store(orow + n, 0LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
       }
     }
@@ -1583,6 +1662,18 @@ bool wg_merge_on() {
   return true;
 #endif
 }
+}  // namespace
+// The FP16 decoder's o_proj fused into the workgroup merge (decoder.cpp
+// oproj_fusable); the tuning build's LLM_OPROJ_FUSE=0 restores the o_proj
+// GEMM launch (A/B, parity).
+bool oproj_fuse_on() {
+#if LLM_TUNING
+  return env_int("LLM_OPROJ_FUSE", 1) != 0;
+#else
+  return true;
+#endif
+}
+namespace {
 int beam_mfma_balance16() {
 #if LLM_TUNING
   static const int v = env_int("LLM_BEAM_MFMA_BALANCE16", 64);
@@ -1609,6 +1700,14 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
   }
   constexpr int ST = split_stages<D, TS, LLM_F16>();
   if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct
+    if constexpr (D <= kOprojMaxD) {
+      if (a.o_acc) {
+        hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
+                                            LLM_F16, true, true, true>),
+                           dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
                                         LLM_F16, true, true>),
                        dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
@@ -1915,7 +2014,12 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   if (plan) *plan = PaPlan{};
   if (B == 0) return LLM_OK;
   const bool row_out = rows && (rows->q || rows->out16);
-  LLM_REQUIRE(plan || (q != nullptr && (out != nullptr || row_out)), "pa_decode: q/out NULL");
+  // the FP16 decoder's fused o_proj (PaRowOutputs::o_acc): workgroup-merge launches only
+  const bool oproj = rows && rows->o_acc && !rows->q && !rows->f32_rows;
+  LLM_REQUIRE(plan || (q != nullptr && (out != nullptr || row_out || oproj)), "pa_decode: q/out NULL");
+  LLM_REQUIRE(!oproj || (rows->wo_heads && rows->o_x && rows->o_n > 0 && D <= kOprojMaxD && H <= 64),
+              "pa_decode: fused o_proj needs W_o head slices, an output, o_n > 0, head_dim <= 128 "
+              "and at most 64 heads");
   LLM_REQUIRE(!rows || !rows->q || rows->inv_scale, "pa_decode: row quantisation needs inv_scale");
   LLM_REQUIRE(!row_out || (size_t)H * D * 4 <= 65536, "pa_decode: row outputs need H*D <= 16384");
   LLM_REQUIRE(!rows || !rows->pack || (H * D) % 64 == 0, "pa_decode: packed row outputs need H*D % 64 == 0");
@@ -1954,7 +2058,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // resident waves (2 / 4 / 8 waves per workgroup: a 6-wave workgroup would
   // leave 2 of the 8 slots idle): C3 6 -> 8 splits
   const bool f32_rows = rows && rows->f32_rows && !rows->q && !rows->out16;
-  const bool wgm_ok = ((row_out && rows->out16 && !rows->q) || f32_rows) && row_group == 1 &&
+  const bool wgm_ok = ((row_out && rows->out16 && !rows->q) || oproj || f32_rows) && row_group == 1 &&
                       kv->kv_dtype == LLM_F16 && wg_merge_on();
   int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident_launch);
   if (wgm_ok && pps_fixed <= 0 && !f32_rows) {
@@ -1969,7 +2073,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
 #if LLM_TUNING
   // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
   // eligible launches (fp16 row outputs, dynamic splits)
-  if (rows && rows->out16 && !rows->q && row_group == 1 && pps_fixed <= 0) {
+  if (rows && (rows->out16 || oproj) && !rows->q && row_group == 1 && pps_fixed <= 0) {
     const int f = env_int("LLM_WGM_SPLITS", 0);
     if (f >= 2 && f <= kWgmMaxSplits && (long long)f * kMaxPps >= ntiles_max) nsplit = f;
   }
@@ -2008,10 +2112,12 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     plan->nsplit = nsplit;
     plan->form = (direct ? LLM_PA_FORM_DIRECT : wg ? LLM_PA_FORM_WG_MERGE
                   : row_out ? LLM_PA_FORM_SPLIT_MERGE_ROW : LLM_PA_FORM_SPLIT_MERGE) |
-                 (beam ? LLM_PA_FORM_BEAM : 0);
+                 (beam ? LLM_PA_FORM_BEAM : 0) | (oproj && wg ? LLM_PA_FORM_OPROJ : 0);
     return LLM_OK;
   }
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
+  if (oproj && (direct || row_group != 1 || nsplit > kWgmMaxSplits || !wgm_ok))
+    return fail(LLM_ERR_UNSUPPORTED, "pa_decode: the fused o_proj needs the workgroup-merge form");
 
   PaSplitArgs a{};
   a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
@@ -2048,6 +2154,12 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     a.out16 = static_cast<_Float16*>(rows->out16);
     a.pack = rows->pack;
     a.out = rows->keep_out || f32_rows ? out : nullptr;
+    if (oproj) {
+      a.o_acc = rows->o_acc;
+      a.o_x = rows->o_x;
+      a.wo_heads = static_cast<const _Float16*>(rows->wo_heads);
+      a.o_n = rows->o_n;
+    }
   }
   hipError_t e;
   bool beam = false;  // the beam kernel ran: every split holds a partial

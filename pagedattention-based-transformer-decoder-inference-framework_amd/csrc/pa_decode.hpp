@@ -21,6 +21,18 @@ struct PaRowOutputs {
   // itself (the INT8 o_proj's quantising prologue), so a split launch may
   // merge its splits inside the workgroup and write `out` (no merge launch)
   int f32_rows = 0;
+  // FP16 decoder, fused o_proj (workgroup-merge launches only, pa_decode_plan
+  // form LLM_PA_FORM_WG_MERGE | LLM_PA_FORM_OPROJ): each (row, head)
+  // workgroup multiplies its merged head (rounded to fp16, as the o_proj
+  // input) by W_o's rows of that head and adds the o_n products into o_acc
+  // row b with atomics (counted fixed point, common.hpp oacc_term; all zero
+  // between launches); the adder completing a column writes o_x[b][n] (fp32,
+  // what the o_proj GEMM would have written) and clears the column.
+  // wo_heads: fp16 [H][D/8][o_n][8] (8 consecutive k of one column per 16 bytes).
+  long long* o_acc = nullptr;
+  float* o_x = nullptr;
+  const void* wo_heads = nullptr;
+  int o_n = 0;
 };
 
 // The launch a call takes (pa_decode_plan): splits per (row, head) and
@@ -39,6 +51,9 @@ int pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, float
                        const PaRowOutputs* rows = nullptr, int row_group = 1,
                        PaPlan* plan = nullptr);
 int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
+// Whether the FP16 decoder fuses its o_proj into the attention's workgroup
+// merge (PaRowOutputs::o_acc); always in the product build.
+bool oproj_fuse_on();
 
 // Split merge of per-(row, head, split) partial softmax states into rows
 // (out fp32 [B][H*D] and/or the rows->q / out16 o_proj inputs); row b's

@@ -36,6 +36,7 @@ pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
 TIE_TOL = 1e-5
 FORM_DIRECT, FORM_SPLIT_MERGE, FORM_SPLIT_MERGE_ROW, FORM_WG_MERGE, FORM_BEAM = 0, 1, 2, 3, 16
+FORM_OPROJ = 32  # FP16 decoder: o_proj fused into the workgroup merge
 
 
 def _torch():
@@ -200,7 +201,7 @@ def test_f16_step_workgroup_merge_vs_oracle(gpu, oracle):
     taps = _Taps(dec, w["cfg"], rows, f16=True)
     dec.begin_synthetic(rows, T, 5, True)
     ns, form = dec.attention_plan()
-    assert form == FORM_WG_MERGE and 2 <= ns <= 8, (ns, form)
+    assert form == FORM_WG_MERGE | FORM_OPROJ and 2 <= ns <= 8, (ns, form)
     odec = OracleDecoder(oracle, w, rows)
     decoder_kv_to_oracle(dec, odec, rows, T)
     logits = torch.empty((rows, V), device="cuda")

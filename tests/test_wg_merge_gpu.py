@@ -46,13 +46,17 @@ def _model(rng, L, H, D, V):
     return {k: np.ascontiguousarray(v) for k, v in w.items()}
 
 
-def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16):
+def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16, fuse=True, taps=False):
     """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`
-    (tuning build: splits > 0 forces the split count)."""
+    (tuning build: splits > 0 forces the split count, fuse=False keeps the
+    o_proj GEMM launch instead of the workgroup merge's fused o_proj).
+    taps=True: also the activation taps of the last step (llm_decoder_set_taps:
+    per layer the four packed fp16 GEMM inputs), as uint16 [L][4][B16 * qa_ld]."""
     import torch
     import llm_capi
     os.environ["LLM_WG_MERGE"] = "1" if wgm else "0"
     os.environ["LLM_WGM_SPLITS"] = str(splits)
+    os.environ["LLM_OPROJ_FUSE"] = "1" if fuse else "0"
     lib.llm_decoder_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_void_p)]
     lib.llm_decoder_set_f16_weights.argtypes = [ctypes.c_void_p, ctypes.POINTER(_F16W)]
     lib.llm_decoder_begin_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -70,6 +74,12 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16):
                                                  "wo", "w1", "w2", "b1", "b2")])
         llm_capi.check(lib.llm_decoder_set_f16_weights(dec, ctypes.byref(ww)), lib)
         llm_capi.check(lib.llm_decoder_begin_synthetic(dec, B, ctx, 77, 1), lib)
+        b16, qa_ld = (B + 15) // 16 * 16, 4 * H * D
+        if taps:
+            tq = torch.zeros((L, 4, b16 * qa_ld), dtype=torch.int16, device="cuda")
+            ts_ = torch.zeros((L * 4 * B,), dtype=torch.float32, device="cuda")
+            lib.llm_decoder_set_taps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+            llm_capi.check(lib.llm_decoder_set_taps(dec, tq.data_ptr(), ts_.data_ptr()), lib)
         rng = np.random.default_rng(5)
         out = []
         logits = torch.empty((B, V), device="cuda")
@@ -79,11 +89,14 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16):
                            lib)
             llm_capi.check(lib.llm_decoder_sync(dec), lib)
             out.append(logits.cpu().numpy().copy())
+        if taps:
+            return np.stack(out), tq.cpu().numpy().view(np.uint16)
         return np.stack(out)
     finally:
         lib.llm_decoder_destroy(dec)
         os.environ.pop("LLM_WG_MERGE", None)
         os.environ.pop("LLM_WGM_SPLITS", None)
+        os.environ.pop("LLM_OPROJ_FUSE", None)
 
 
 @pytest.mark.parametrize("H,D,ts", [(12, 64, 16), (8, 128, 16), (4, 256, 16), (8, 128, 32)],
@@ -101,10 +114,54 @@ def test_wg_merge_bitwise(gpu, ctx, H, D, ts):
     L, V, S, B = 2, 512, 2100, 16
     w = _model(np.random.default_rng(3), L, H, D, V)
     for ns in ((3, 5, 8) if D == 64 else (3, 8)):
-        on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, ns, ts)
-        off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False, ns, ts)
+        on = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, ns, ts, fuse=False)
+        off = _run(tune, w, L, H, D, V, S, B, ctx, 3, False, ns, ts, fuse=False)
         assert np.isfinite(on).all()
         assert np.array_equal(on.view(np.uint32), off.view(np.uint32)), (ns, np.abs(on - off).max())
     auto = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, 0, ts)
     prod = _run(llm_capi.load(), w, L, H, D, V, S, B, ctx, 3, True, 0, ts)
     assert np.array_equal(prod.view(np.uint32), auto.view(np.uint32))
+
+
+@pytest.mark.parametrize("H,D,ts", [(12, 64, 16), (8, 128, 16), (8, 128, 32)],
+                         ids=["c2_width_d64", "d128", "d128_page32"])
+@pytest.mark.parametrize("ctx", [1500, 40])
+def test_fused_oproj(gpu, ctx, H, D, ts):
+    """The o_proj fused into the workgroup merge (each (row, head) workgroup
+    adds o_h . W_o[h rows] into counted int64 fixed-point columns; the adder
+    completing a column writes x and clears it) against the o_proj GEMM
+    launch at the same split count: step-0 logits within 1e-3, tensor-
+    normalised (fp32 sums in another order plus 2^-33 per head of fixed-point
+    rounding, moved across the fp16 roundings of the next GEMM inputs now and
+    then; the elementwise oracle bound is checked teacher-forced,
+    test_decoder_gpu.py); bit-identical from run to run (the integer sum does
+    not depend on the order the heads' atomics land in) over several steps
+    (every layer's columns cleared for the next); and, through the taps, the
+    same o_proj input and an fc1 input within one fp16 ulp."""
+    import llm_capi
+    from _util import rel_err
+    tune = llm_capi.load_tune()
+    L, V, S, B = 2, 512, 2100, 16
+    w = _model(np.random.default_rng(4), L, H, D, V)
+    for ns in (3, 8):
+        fused = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True)
+        again = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True)
+        gemm = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=False)
+        assert np.isfinite(fused).all()
+        assert np.array_equal(fused.view(np.uint32), again.view(np.uint32)), ns
+        assert rel_err(fused[0], gemm[0]) < 1e-3, (ns, rel_err(fused[0], gemm[0]))
+        assert not np.array_equal(fused.view(np.uint32), gemm.view(np.uint32))  # the fused form ran
+        # one step with taps: layer 0's attention output (the o_proj input) is
+        # the same bits, and fc1's input LN2(x) -- x the o_proj output, rounded
+        # to fp16 -- differs in a few elements by one fp16 ulp (or, where
+        # x - mean cancels, by 1e-5 of the tensor's largest value)
+        _, tf = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True)
+        _, tg = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=False, taps=True)
+        hid = H * D
+        n16 = (B + 15) // 16 * 16 * hid
+        assert np.array_equal(tf[0, 1, :n16], tg[0, 1, :n16])
+        fa = tf[0, 2, :n16].view(np.float16).astype(np.float64)
+        fg = tg[0, 2, :n16].view(np.float16).astype(np.float64)
+        bound = np.spacing(np.abs(fg).astype(np.float16)).astype(np.float64) + 1e-5 * np.abs(fg).max()
+        assert np.all(np.abs(fa - fg) <= bound), np.max(np.abs(fa - fg) / bound)
+        assert np.mean(fa != fg) < 0.05, np.mean(fa != fg)
