@@ -2229,7 +2229,7 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
                               void* workspace, size_t workspace_bytes, void* stream) {
   LLM_REQUIRE(kv && (kv->head_dim == 128 || kv->head_dim == 64) && kv->page_size == 16 &&
                   H == kv->num_heads,
-              "pa_decode_tune: D 128 (variants 0-13) or 64 (20-25), page 16 only");
+              "pa_decode_tune: D 128 (variants 0-19) or 64 (20-25), page 16 only");
   const int D = kv->head_dim;
   LLM_REQUIRE((D == 128) == (variant < 20), "pa_decode_tune: variant / head_dim mismatch");
   const int ntiles_max = std::max(1, (T + 15) / 16);
@@ -2268,6 +2268,15 @@ extern "C" int pa_decode_tune(int variant, const pa_kv_view* kv, const float* q,
     case 12: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 32768, 2, 2, 0, true>), grid, block, 0, st, a); break;
     // 13: variant 1 without the full-page fast path (every token takes the validity selects)
     case 13: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 2, 2, 0, false, false, LLM_F16, false>), grid, block, 0, st, a); break;
+    // 14-18: variant 1 with other cache-policy bits of the KV loads (gfx940-family
+    // CPol: sc0 = 1, nt = 2, sc1 = 16): 14 sc0|nt, 15 sc1|nt, 16 sc0|sc1|nt,
+    // 17 sc1, 18 sc0; 19: loads only with sc1|nt
+    case 14: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 3>), grid, block, 0, st, a); break;
+    case 15: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 18>), grid, block, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 19>), grid, block, 0, st, a); break;
+    case 17: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 16>), grid, block, 0, st, a); break;
+    case 18: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 1>), grid, block, 0, st, a); break;
+    case 19: hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 16384, 18, 2, 0, true>), grid, block, 0, st, a); break;
     // D = 64 (C2): 20 production, 21 one 16 KiB stage, 22 8 KiB stages, 23 one
     // 32 KiB stage, 24 / 25 loads only (16 KiB x 2, 32 KiB x 1)
     case 20: hipLaunchKernelGGL((pa_split_kernel<64, 16, false, 16384, 2, 2>), grid, block, 0, st, a); break;

@@ -82,7 +82,7 @@ for r in range(args.rounds):
                                                   llm_capi.ptr(ws), ws_bytes, st))
             run()
             torch.cuda.synchronize()
-            if r == 0 and (v < 10 or v >= 13):  # variants 10-12 are load-only ceilings
+            if r == 0 and (v < 10 or 13 <= v < 19 or v >= 20) and v not in (24, 25):  # load-only ceilings: 10-12, 19, 24, 25
                 err = (out - ref).abs().max().item() / ref.abs().max().item()
                 assert err < 1e-5, (v, pps, err)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
