@@ -153,13 +153,12 @@ constexpr int kKvLoadAux = 2;
 // WGM: the workgroup-merge form (PaSplitArgs::wgm): blockDim = 64 * nsplit,
 // one workgroup per (b, h), wave w = split w.
 // OPROJ (WGM only): the fused o_proj of the FP16 decoder (PaSplitArgs::o_acc).
-// vblock: the workgroup's work item (blockIdx.x, or one item of a persistent
-// workgroup's list: pa_wgm_persist_kernel).
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
-          int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          bool PERSIST = false>
-__device__ __forceinline__ void pa_split_body(const PaSplitArgs& a, int vblock) {
+          int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false>
+__global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
+__attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
+void pa_split_kernel(PaSplitArgs a) {
   constexpr int ES = kv_elem_bytes<KVT>();
   constexpr int EPL = 16 / ES;  // elements per lane per 16-byte load
   constexpr int LPT = D / EPL;
@@ -173,7 +172,7 @@ __device__ __forceinline__ void pa_split_body(const PaSplitArgs& a, int vblock) 
   static_assert(!(WGM && (DIRECT || BEAM)), "the workgroup merge is a split form");
   static_assert(!OPROJ || (WGM && KVT == LLM_F16), "the fused o_proj is a workgroup-merge form");
   const int lane = lane_id();
-  const int wid = vblock * (WGM ? a.nsplit : 4) + wave_id_uniform();
+  const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
   const int G = BEAM ? 4 : WGM ? 1 : a.group;
   const int gi = wid % G;  // row within the group (fastest: adjacent waves)
   const int rest = wid / G;
@@ -516,9 +515,6 @@ __device__ __forceinline__ void pa_split_body(const PaSplitArgs& a, int vblock) 
     // so the o_proj input is bit-identical to the split + merge launches'.
     __shared__ float wg_ml[kWgmMaxSplits][2];
     __shared__ __attribute__((aligned(16))) float wg_acc[kWgmMaxSplits][D];
-    // a persistent workgroup's previous item: wave 0 has read wg_acc / wg_ml
-    // (and, OPROJ, every wave wg_o) before anyone overwrites them
-    if constexpr (PERSIST) __syncthreads();
     if (lane < LPT) {
 #pragma unroll
       for (int e = 0; e < EPL; e += 4)
@@ -674,36 +670,6 @@ __device__ __forceinline__ void pa_split_body(const PaSplitArgs& a, int vblock) 
     }
   }
 }
-
-template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
-          int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
-          int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false>
-__global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
-__attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
-void pa_split_kernel(PaSplitArgs a) {
-  pa_split_body<D, TS, DIRECT, CHUNK_BYTES, AUX, STAGES, MIN_WAVES, LOAD_ONLY, BEAM, KVT, FULLPATH,
-                WGM, OPROJ>(a, blockIdx.x);
-}
-
-// Persistent workgroup-merge launch (tuning build only, LLM_WGM_PERSIST=1): a
-// grid of at most the resident workgroup count, each workgroup taking (b, h)
-// items blockIdx.x, + gridDim.x, ...  When B*H exceeds one resident round (C3:
-// 1024 items on 256 CUs), the waves of a workgroup start their next item as
-// soon as their split of the current one is in LDS, while wave 0 merges it,
-// instead of the CU waiting for the workgroup to drain and the next one to be
-// dispatched.  Bit-identical (tests/test_wgm_persist_gpu.py); not faster:
-// the launch alone ties (631.7-632.3 vs 631.4-632.6 us) and the C3 step
-// loses 0.66 % (3,854 -> 3,829 tok/s, same box, three rounds,
-// profiles/r03/wgm_persist_ab.txt).
-#if LLM_TUNING
-template <int D, int TS, int STAGES, bool OPROJ>
-__global__ __launch_bounds__(64 * kWgmMaxSplits) void pa_wgm_persist_kernel(PaSplitArgs a) {
-  const int items = a.B * a.H;
-  for (int vb = blockIdx.x; vb < items; vb += gridDim.x)
-    pa_split_body<D, TS, false, 16384, kKvLoadAux, STAGES, 0, false, false, LLM_F16, true, true,
-                  OPROJ, true>(a, vb);
-}
-#endif
 
 #if LLM_TUNING
 // Beam-group attention, one WAVE per (group of 4 beams, head, split): the
@@ -1599,32 +1565,6 @@ constexpr int split_stages() {
   return TS * D * kv_elem_bytes<KVT>() > 8192 ? 1 : 2;
 }
 
-// Grid of a workgroup-merge launch over `items` (b, h) workgroups of `threads`:
-// `items` (one workgroup per item: the product), or in the tuning build with
-// LLM_WGM_PERSIST=1 and more items than one resident round, the resident
-// workgroup count, each persistent workgroup then taking items blockIdx.x +
-// k * gridDim.x (pa_wgm_persist_kernel; measured slower, kept for the A/B).
-#if LLM_TUNING
-template <typename K>
-int wgm_persist_grid(K kernel, int items, int threads) {
-  if (env_int("LLM_WGM_PERSIST", 0) == 0) return items;
-  static int cus = 0;
-  int dev = 0, blocks = 0;
-  if (!cus && (hipGetDevice(&dev) != hipSuccess ||
-               hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)) {
-    (void)hipGetLastError();
-    cus = 0;
-    return items;
-  }
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, kernel, threads, 0) != hipSuccess ||
-      blocks <= 0 || cus <= 0) {
-    (void)hipGetLastError();
-    return items;
-  }
-  return (int)std::min<long long>(items, (long long)cus * blocks);
-}
-#endif
-
 template <int D, int TS, bool DIRECT, int KVT>
 long long resident_waves() {
   static long long cached = 0;
@@ -1760,32 +1700,17 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
   }
   constexpr int ST = split_stages<D, TS, LLM_F16>();
   if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct
-    const int items = a.B * a.H, threads = 64 * a.nsplit;
     if constexpr (D <= kOprojMaxD) {
       if (a.o_acc) {
-#if LLM_TUNING
-        const int g = wgm_persist_grid(pa_wgm_persist_kernel<D, TS, ST, true>, items, threads);
-        if (g < items) {
-          hipLaunchKernelGGL((pa_wgm_persist_kernel<D, TS, ST, true>), dim3(g), dim3(threads), 0, st, a);
-          return hipGetLastError();
-        }
-#endif
         hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
                                             LLM_F16, true, true, true>),
-                           dim3(items), dim3(threads), 0, st, a);
+                           dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
         return hipGetLastError();
       }
     }
-#if LLM_TUNING
-    const int g = wgm_persist_grid(pa_wgm_persist_kernel<D, TS, ST, false>, items, threads);
-    if (g < items) {
-      hipLaunchKernelGGL((pa_wgm_persist_kernel<D, TS, ST, false>), dim3(g), dim3(threads), 0, st, a);
-      return hipGetLastError();
-    }
-#endif
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
                                         LLM_F16, true, true>),
-                       dim3(items), dim3(threads), 0, st, a);
+                       dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
     return hipGetLastError();
   }
 #if LLM_TUNING

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL: the persistent kernel and tests/test_wgm_persist_gpu.py were removed after this
+# measurement (profiles/r03/wgm_persist_ab.txt); kept as the record of how it was run.
 # Persistent workgroup-merge attention: parity (bitwise vs one workgroup per
 # item, and the WGM / decoder suites), then a same-box C3 A/B against the
 # previous product library in ab_old/.
