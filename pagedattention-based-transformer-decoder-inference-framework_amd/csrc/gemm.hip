@@ -640,6 +640,7 @@ hipError_t launch_gemm_mt(const GemmArgs& a, int NT, int waves, int mblocks, hip
                           int kslices) {
 #if LLM_TUNING
   if (NT == 4 && !a.ln_x) return launch_gemm_nt<KIND, MT, 4>(a, waves, mblocks, st, kslices);
+  if (NT == 3 && !a.ln_x) return launch_gemm_nt<KIND, MT, 3>(a, waves, mblocks, st, kslices);
 #endif
   return NT == 2 ? launch_gemm_nt<KIND, MT, 2>(a, waves, mblocks, st, kslices)
                  : launch_gemm_nt<KIND, MT, 1>(a, waves, mblocks, st, kslices);
@@ -675,6 +676,13 @@ struct TileChoice {
 };
 // By shape: M rows, N columns, K inputs (the LayerNorm-prologue and split-K
 // launches keep their own forms).
+// Measured and not taken (round 3): C3's qkv (384 column tiles, 64 rows) as
+// 3 column tiles x 32 rows x 8 waves (tuning build NT 3), 128 column blocks x
+// 2 row blocks = 256 workgroups, each reading 96 KB of weights + 64 KB of A
+// instead of 64 + 128 KB.  Standalone, weights from HBM (scripts/tune_gemm.py
+// --nts 1 2 3, profiles/r03/gemm_nt3.txt) 9.32 -> 7.93 us, but in the C3 step
+// (KV-append epilogue, same box, three rounds) 3,846-3,849 -> 3,840-3,845
+// tok/s, parity green (profiles/r03/gemm_nt3_ab.txt).
 inline bool narrow_tile_for(int M, int N, int K, TileChoice& t) {
   if (M <= 16 || M > 64) return false;
   const int ntiles = (N + 15) / 16;

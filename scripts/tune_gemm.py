@@ -18,6 +18,8 @@ ap.add_argument("--M", type=int, default=64)
 ap.add_argument("--reps", type=int, default=50)
 ap.add_argument("--hid", type=int, default=2048)
 ap.add_argument("--copies", type=int, default=8)
+ap.add_argument("--nts", type=int, nargs="*", default=[1, 2])
+ap.add_argument("--only", default="")
 args = ap.parse_args()
 lib = llm_capi.load_tune()  # tuning build: `make tune`
 lib.i8_gemm_tune.restype = ctypes.c_int
@@ -31,6 +33,8 @@ shapes = [("qkv_proj", hid, 3 * hid), ("o_proj", hid, hid), ("mlp_fc1", hid, 4 *
 s = torch.cuda.Stream()
 
 for name, K, N in shapes:
+    if args.only and name not in args.only.split(","):
+        continue
     W = torch.randint(-128, 128, (K, N), dtype=torch.int8, device="cuda")
     Wp = llm_capi.pack_weights(W, llm_capi.LLM_I8)
     # distinct weight copies so consecutive launches stream from HBM, not L2/MALL
@@ -44,7 +48,7 @@ for name, K, N in shapes:
     Ap = llm_capi.pack_weights(A.t().contiguous(), llm_capi.LLM_I8)  # A-fragment order
     llm_capi.check(lib.i8_gemm_tune(1, 8, 0, 0, A.data_ptr(), K, Wp.data_ptr(),
                                     ref.data_ptr(), M, N, K, sa.data_ptr(), sw.data_ptr(), None))
-    grid = [(nt, w, 1, mr) for nt in (1, 2) for w in (4, 8) for mr in (16, 32, 64)
+    grid = [(nt, w, 1, mr) for nt in args.nts for w in (4, 8) for mr in (16, 32, 64)
             if mr >= 16 * ((M + 63) // 64) or mr < M or mr == 16]
     for nt, ks, apk, mr in grid:
         for _ in range(1):

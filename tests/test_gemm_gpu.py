@@ -61,6 +61,7 @@ def test_i8_gemm_no_scales(gpu, oracle):
 @pytest.mark.parametrize("M,K,N,nt,waves", [
     (64, 2048, 6144, 2, 8), (64, 8192, 2048, 1, 8), (64, 2048, 2048, 1, 16), (37, 512, 96, 2, 8),
     (16, 256, 64, 1, 8), (100, 1024, 512, 2, 16), (64, 8192, 2048, 4, 4), (48, 2048, 2048, 4, 8),
+    (64, 2048, 6144, 3, 8), (40, 2048, 6144, 3, 8),  # C3's qkv form: 3 column tiles
     (512, 1024, 768, 0, 0), (300, 512, 4096, 0, 0),  # prefill-chunk row counts
 ])
 def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
