@@ -28,7 +28,10 @@ enum llm_status {
   LLM_ERR_UNSUPPORTED = 2,  /* valid request this build does not implement (e.g. top-k in attention) */
   LLM_ERR_HIP = 3,          /* HIP runtime error */
   LLM_ERR_OOM = 4,          /* device or page-pool allocation failure */
-  LLM_ERR_IO = 5            /* weight / cache file I/O */
+  LLM_ERR_IO = 5,           /* weight / cache file I/O */
+  LLM_ERR_RANGE = 6         /* a device value left a fixed-point accumulator's range (the
+                               FP16 decoder's fused o_proj); reported by llm_decoder_sync /
+                               a synchronous step, cleared by the next begin / generate */
 };
 
 /* Element types.  KV pools may be any of the four (the T of
@@ -427,7 +430,19 @@ int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_width, int sh
  * stream NULL -> the decoder's own stream. */
 int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
                      int32_t* next_host, void* stream);
+/* Wait for the device.  LLM_ERR_RANGE if, since the last begin / generate, a
+ * step's fused o_proj (FP16 decoders, LLM_PA_FORM_OPROJ) met a head product
+ * outside its fixed-point range ((2^23 - 1) / num_heads in magnitude, or not
+ * finite): that product was clamped, so the affected x values are wrong, but
+ * the accumulator columns stayed consistent and later steps are unaffected by
+ * it.  A step with next_host reports the same. */
 int llm_decoder_sync(llm_decoder* d);
+/* Health of the fused o_proj after waiting for the device: *clamped = 1 if a
+ * term was clamped since the last begin / generate (see llm_decoder_sync),
+ * *nonzero_columns = accumulator columns not back at zero (0 between steps
+ * unless a launch was interrupted).  Either pointer may be NULL.  Decoders
+ * without the fused o_proj report 0 / 0. */
+int llm_decoder_oproj_status(llm_decoder* d, int* clamped, long long* nonzero_columns);
 /* Enqueue on `stream` (NULL: the decoder's) a device copy of the last step's
  * next ids (int32 [batch], the greedy argmax or the sampled ids) to dst_dev:
  * the ids-only gather of the multi-GPU path without a host sync. */
@@ -459,7 +474,10 @@ int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form);
 /* Enqueue layer `layer`'s attention launch of the decoder's step on `stream`
  * (NULL: the decoder's) -- the same kernels, grid and outputs as inside the
  * step graph (q from the last step's projection, each row's live context, the
- * o_proj input written), for timing the step's own launch in isolation. */
+ * o_proj input written), for timing the step's own launch in isolation.  The
+ * fused o_proj of an FP16 decoder accumulates into a scratch set of columns of
+ * its own here (not the step's), so a run may overlap an in-flight step; two
+ * runs of one decoder must not overlap each other. */
 int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream);
 int llm_decoder_context_len(const llm_decoder* d, int row);
 kv_cache* llm_decoder_kv(llm_decoder* d);

@@ -228,6 +228,16 @@ class Decoder {
     py::gil_scoped_release nogil;
     check(llm_decoder_run_attention(d_, layer, reinterpret_cast<void*>(stream)));
   }
+  // llm_decoder_oproj_status: (range guard tripped, accumulator columns not at zero)
+  py::tuple oproj_status() {
+    int clamped = 0;
+    long long nz = 0;
+    {
+      py::gil_scoped_release nogil;
+      check(llm_decoder_oproj_status(d_, &clamped, &nz));
+    }
+    return py::make_tuple(clamped != 0, nz);
+  }
   // llm_decoder_attention_plan: (splits per (row, head), LLM_PA_FORM_*)
   py::tuple attention_plan() {
     int ns = 0, form = 0;
@@ -436,6 +446,7 @@ PYBIND11_MODULE(llm_decoder, m) {
         .def("copy_next_ids", &Decoder::copy_next_ids, py::arg("dst_ptr"), py::arg("stream") = 0)
         .def("context_len", &Decoder::context_len)
         .def("attention_plan", &Decoder::attention_plan)
+        .def("oproj_status", &Decoder::oproj_status)
         .def("run_attention", &Decoder::run_attention, py::arg("layer") = 0,
              py::arg("stream") = 0)
         .def_property_readonly("kv_handle", &Decoder::kv_handle);

@@ -58,10 +58,24 @@ constexpr float kLog2e = 1.4426950408889634f;
 // whose returned old value counts H - 1 arrivals holds the complete sum: it
 // stores the fp32 value and clears the column for the next layer.  Exact to
 // 2^-33 per head for |sum| < 2^23 (8.4e6) and H <= 64.
+//
+// Range guard: the count bits stay intact only while |sum| < 2^23.  Each
+// head's term is therefore clamped to |v| <= oacc_limit(H) = (2^23 - 1) / H,
+// so H terms can never reach 2^23, and a NaN maps to the positive limit.  A
+// clamped term sets *flag (a plain vector store; the decoder turns it into
+// LLM_ERR_RANGE at llm_decoder_sync / the next synchronous step).  The
+// column then still completes after exactly H arrivals and is cleared, so an
+// out-of-range value costs that one output, never the later layers or steps.
 constexpr float kOAccScale = 4294967296.f;  // 2^32
 constexpr long long kOAccCount = 1LL << 56;
-__device__ __forceinline__ long long oacc_term(float v) {
-  return __float2ll_rn(v * kOAccScale) + kOAccCount;
+__host__ __device__ __forceinline__ float oacc_limit(int H) {
+  return (float)((1 << 23) - 1) / (float)H;
+}
+__device__ __forceinline__ long long oacc_term(float v, float lim, bool& clamped) {
+  const bool ok = fabsf(v) <= lim;  // false for NaN and +-inf
+  clamped = !ok;
+  const float c = ok ? v : (v < 0.f ? -lim : lim);
+  return __float2ll_rn(c * kOAccScale) + kOAccCount;
 }
 __device__ __forceinline__ int oacc_count(long long v) {
   return (int)((v + (kOAccCount >> 1)) >> 56);

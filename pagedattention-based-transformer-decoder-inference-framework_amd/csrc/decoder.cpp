@@ -91,8 +91,14 @@ struct llm_decoder {
   DevBuf<int8_t> qa;
   DevBuf<uint16_t> a16;
   // FP16: the fused o_proj's int64 columns [max_batch][hid] (zero between
-  // attention launches: the adder completing a column clears it)
-  DevBuf<long long> oacc;
+  // attention launches: the adder completing a column clears it); oacc_run:
+  // llm_decoder_run_attention's own set (allocated on first use), so a timed
+  // run never mixes its arrivals with an in-flight step's; oflag: the range
+  // guard's device flag (common.hpp oacc_term), h_oflag its pinned host copy
+  DevBuf<long long> oacc, oacc_run;
+  DevBuf<int> oflag;
+  int* h_oflag = nullptr;
+  int oproj_range_status();
   DevBuf<int32_t> tokens, pos, ctx;
   DevBuf<uint8_t> attn_ws;
   size_t attn_ws_bytes = 0;
@@ -113,6 +119,7 @@ struct llm_decoder {
   LnSource embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
 
   ~llm_decoder() {
+    if (h_oflag) (void)hipHostFree(h_oflag);
     if (graph) (void)hipGraphExecDestroy(graph);
     if (kv) kv_cache_destroy(kv);
     if (stream) (void)hipStreamDestroy(stream);
@@ -200,6 +207,10 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
     RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
     RET_IF(d->oacc.alloc((size_t)B * hid));
     LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * B * hid));
+    RET_IF(d->oflag.alloc(1));
+    LLM_HIP_RET(hipMemset(d->oflag.p, 0, sizeof(int)));
+    LLM_HIP_RET(hipHostMalloc(reinterpret_cast<void**>(&d->h_oflag), sizeof(int)));
+    *d->h_oflag = 0;
   }
   d->b16 = B16;
   RET_IF(d->tokens.alloc((size_t)B));
@@ -323,7 +334,12 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
   RET_IF(upload_common(d, w->emb, w->ln1_g, w->ln1_b, w->ln2_g, w->ln2_b));
   RET_IF(upload_packed(d->wqkv, d->sz_qkv, w->wqkv, L, hid, 3 * hid, LLM_F16, "wqkv"));
   RET_IF(upload_packed(d->wo, d->sz_o, w->wo, L, hid, hid, LLM_F16, "wo"));
-  if (d->D % 8 == 0 && d->D <= 128) {  // the fused o_proj's head slices: [h][kg][n][j] = W_o[h D + 8 kg + j][n]
+  // the fused o_proj's head slices: [h][kg][n][j] = W_o[h D + 8 kg + j][n] (a
+  // second copy of W_o, L * hid^2 fp16), only where the fused o_proj can run
+  // (oproj_fusable); the step then reads these instead of the packed W_o, so
+  // the bytes a step streams (w_keep_for) are unchanged
+  d->wo_heads.alloc(0);
+  if (d->D % 8 == 0 && d->D <= 128 && d->H <= 64 && oproj_fuse_on()) {
     const int D = d->D, KG = D / 8;
     const uint16_t* src = static_cast<const uint16_t*>(w->wo);
     std::vector<uint16_t> sl((size_t)hid * hid);
@@ -507,6 +523,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
     ro.o_x = R.oproj_out;
     ro.wo_heads = wo_heads.p + (size_t)l * hid * hid;
     ro.o_n = hid;
+    ro.o_flag = oflag.p;
     ro.out16 = tap_q ? R.act : nullptr;  // the taps read the packed o_proj input
   } else {
     ro.out16 = R.act;
@@ -705,8 +722,24 @@ int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t
   if (next_host) {
     LLM_HIP_RET(hipMemcpyAsync(next_host, tokens.p, sizeof(int32_t) * batch,
                                hipMemcpyDeviceToHost, st));
+    if (oflag.p)
+      LLM_HIP_RET(hipMemcpyAsync(h_oflag, oflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
     LLM_HIP_RET(hipStreamSynchronize(st));
+    if (oflag.p && *h_oflag) return oproj_range_status();
   }
+  return LLM_OK;
+}
+
+// LLM_ERR_RANGE once the fused o_proj's range flag is set (common.hpp
+// oacc_term); the flag stays set until reset_rows.
+int llm_decoder::oproj_range_status() {
+  if (!oflag.p) return LLM_OK;
+  LLM_HIP_RET(hipMemcpy(h_oflag, oflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (*h_oflag)
+    return fail(LLM_ERR_RANGE,
+                "decoder: a head product of the fused o_proj left its fixed-point range "
+                "(|v| > (2^23 - 1) / num_heads, or not finite) and was clamped; the affected "
+                "hidden values of that step are wrong");
   return LLM_OK;
 }
 
@@ -802,6 +835,7 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   d->h_pos.assign(d->maxB, 0);
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
   if (d->oacc.p) LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * d->oacc.n));
+  if (d->oflag.p) LLM_HIP_RET(hipMemset(d->oflag.p, 0, sizeof(int)));
   std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
   LLM_HIP_RET(hipMemcpy(d->pos.p, pos.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
   LLM_HIP_RET(hipMemcpy(d->ctx.p, ctx.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
@@ -927,9 +961,35 @@ extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream
   LLM_REQUIRE(layer >= 0 && layer < d->L, "llm_decoder_run_attention: layer out of range");
   hipStream_t st = stream ? as_stream(stream) : d->stream;
   Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
-  // the step's fused o_proj writes the attention rows' fp32 buffer here, not x
-  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.o;
+  // the step's fused o_proj writes the attention rows' fp32 buffer here, not
+  // x, and accumulates into columns of its own (oacc_run: zero at allocation,
+  // and every completed column clears itself, as the step's do)
+  if (d->oproj_fusable(R)) {
+    if (!d->oacc_run.p) {
+      RET_IF(d->oacc_run.alloc(d->oacc.n));
+      LLM_HIP_RET(hipMemset(d->oacc_run.p, 0, sizeof(long long) * d->oacc_run.n));
+    }
+    R.oacc = d->oacc_run.p, R.oproj_out = R.o;
+  }
   return d->layer_attn(layer, st, R);
+}
+
+extern "C" int llm_decoder_oproj_status(llm_decoder* d, int* clamped, long long* nonzero_columns) {
+  LLM_REQUIRE(d, "llm_decoder_oproj_status: NULL");
+  std::lock_guard<std::mutex> g(d->mu);
+  LLM_HIP_RET(hipDeviceSynchronize());
+  int f = 0;
+  long long nz = 0;
+  if (d->oflag.p) LLM_HIP_RET(hipMemcpy(&f, d->oflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  for (const DevBuf<long long>* b : {&d->oacc, &d->oacc_run}) {
+    if (!b->p) continue;
+    std::vector<long long> h(b->n);
+    LLM_HIP_RET(hipMemcpy(h.data(), b->p, sizeof(long long) * b->n, hipMemcpyDeviceToHost));
+    for (long long v : h) nz += v != 0;
+  }
+  if (clamped) *clamped = f;
+  if (nonzero_columns) *nonzero_columns = nz;
+  return LLM_OK;
 }
 
 extern "C" int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
@@ -953,7 +1013,7 @@ extern "C" int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* str
 extern "C" int llm_decoder_sync(llm_decoder* d) {
   LLM_REQUIRE(d, "llm_decoder_sync: NULL");
   LLM_HIP_RET(hipDeviceSynchronize());
-  return LLM_OK;
+  return d->oproj_range_status();
 }
 
 extern "C" int llm_decoder_context_len(const llm_decoder* d, int row) {

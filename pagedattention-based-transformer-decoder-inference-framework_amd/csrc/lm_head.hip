@@ -400,7 +400,10 @@ int cu_count() {
 
 int lm_head_tiles(int V) {
 #if LLM_TUNING
-  const int forced = env_int("LLM_LM_TILES", 0);  // tuning build: A/B of the tiles per workgroup
+  // tuning build: A/B of the tiles per workgroup.  Read once per process: a
+  // decoder sizes its argmax partials (lm_nwg) at create, so the value must
+  // not change under it between create and a launch.
+  static const int forced = env_int("LLM_LM_TILES", 0);
   if (forced >= 1 && forced <= kLmWaves) return forced;
 #endif
   const int ntiles = (V + 15) / 16;

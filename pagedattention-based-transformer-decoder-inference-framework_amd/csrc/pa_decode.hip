@@ -84,6 +84,7 @@ struct PaSplitArgs {
   float* o_x;
   const _Float16* wo_heads;  // [H][D/8][o_n][8]
   int o_n;
+  int* o_flag;  // set to 1 when a head's term was clamped (common.hpp oacc_term)
 };
 
 constexpr int kWgmMaxSplits = 8;  // one merge batch (pa_merge_row_kernel's kMergeBatch)
@@ -613,6 +614,8 @@ void pa_split_kernel(PaSplitArgs a) {
       __syncthreads();
       long long* orow = a.o_acc + (size_t)b * o_n;
       const f16x2* op = reinterpret_cast<const f16x2*>(wg_o);
+      const float olim = oacc_limit(a.H);
+      bool clamped = false;
       for (int base = ocol0; base < o_n; base += CF * ostride) {
         if (base != ocol0) load_round(base);
         float pj[CF];
@@ -632,7 +635,9 @@ void pa_split_kernel(PaSplitArgs a) {
 #pragma unroll
         for (int j = 0; j < CF; ++j) {
           const int n = base + j * ostride;
-          tj[j] = oacc_term(pj[j]);
+          bool cj;
+          tj[j] = oacc_term(pj[j], olim, cj);
+          clamped |= cj && n < o_n;
           oj[j] = n < o_n ? (long long)atomicAdd(reinterpret_cast<unsigned long long*>(orow + n),
                                                  (unsigned long long)tj[j])
                           : 0;
@@ -646,6 +651,7 @@ void pa_split_kernel(PaSplitArgs a) {
           }
         }
       }
+      if (clamped) *a.o_flag = 1;
     }
     return;
   }
@@ -2017,9 +2023,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // the FP16 decoder's fused o_proj (PaRowOutputs::o_acc): workgroup-merge launches only
   const bool oproj = rows && rows->o_acc && !rows->q && !rows->f32_rows;
   LLM_REQUIRE(plan || (q != nullptr && (out != nullptr || row_out || oproj)), "pa_decode: q/out NULL");
-  LLM_REQUIRE(!oproj || (rows->wo_heads && rows->o_x && rows->o_n > 0 && D <= kOprojMaxD && H <= 64),
-              "pa_decode: fused o_proj needs W_o head slices, an output, o_n > 0, head_dim <= 128 "
-              "and at most 64 heads");
+  LLM_REQUIRE(!oproj || (rows->wo_heads && rows->o_x && rows->o_flag && rows->o_n > 0 &&
+                         D <= kOprojMaxD && H <= 64),
+              "pa_decode: fused o_proj needs W_o head slices, an output, a range flag, o_n > 0, "
+              "head_dim <= 128 and at most 64 heads");
   LLM_REQUIRE(!rows || !rows->q || rows->inv_scale, "pa_decode: row quantisation needs inv_scale");
   LLM_REQUIRE(!row_out || (size_t)H * D * 4 <= 65536, "pa_decode: row outputs need H*D <= 16384");
   LLM_REQUIRE(!rows || !rows->pack || (H * D) % 64 == 0, "pa_decode: packed row outputs need H*D % 64 == 0");
@@ -2159,6 +2166,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
       a.o_x = rows->o_x;
       a.wo_heads = static_cast<const _Float16*>(rows->wo_heads);
       a.o_n = rows->o_n;
+      a.o_flag = rows->o_flag;
     }
   }
   hipError_t e;

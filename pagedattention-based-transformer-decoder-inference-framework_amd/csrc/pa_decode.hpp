@@ -33,6 +33,9 @@ struct PaRowOutputs {
   float* o_x = nullptr;
   const void* wo_heads = nullptr;
   int o_n = 0;
+  // device int set to 1 when a head's term left the accumulator's range and was
+  // clamped (common.hpp oacc_term); required with o_acc
+  int* o_flag = nullptr;
 };
 
 // The launch a call takes (pa_decode_plan): splits per (row, head) and

@@ -19,7 +19,8 @@ HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "libllm_decoder_hip.so"
 TUNE_LIB_PATH = HERE / "libllm_decoder_hip_tune.so"  # `make tune`: A/B hooks, never the product
 
-LLM_OK, LLM_ERR_INVALID, LLM_ERR_UNSUPPORTED, LLM_ERR_HIP, LLM_ERR_OOM, LLM_ERR_IO = range(6)
+(LLM_OK, LLM_ERR_INVALID, LLM_ERR_UNSUPPORTED, LLM_ERR_HIP, LLM_ERR_OOM, LLM_ERR_IO,
+ LLM_ERR_RANGE) = range(7)
 LLM_F16, LLM_I8, LLM_F32, LLM_BF16 = 0, 1, 2, 3
 LLM_ACT_NONE, LLM_ACT_RELU, LLM_ACT_GELU = 0, 1, 2
 
@@ -115,6 +116,8 @@ _SIGS = {
     "kv_cache_save_tiles": (c_int, [c_void_p, c_int, c_int, ctypes.c_char_p]),
     "kv_cache_load_tiles": (c_int, [c_void_p, c_int, c_int, ctypes.c_char_p]),
     "kv_tiles_inspect": (c_int, [ctypes.c_char_p, ctypes.c_longlong, ctypes.POINTER(c_int)]),
+    "llm_decoder_oproj_status": (c_int, [c_void_p, ctypes.POINTER(c_int),
+                                         ctypes.POINTER(ctypes.c_longlong)]),
 }
 
 _lib = None

@@ -151,6 +151,55 @@ def test_int8_step_multi_split_attention_vs_oracle(gpu, oracle, rows, T, form):
           f"logits rel err {worst:.2e}")
 
 
+@pytest.mark.timeout(600)
+def test_int8_c3_shipped_launch_vs_oracle(gpu, oracle):
+    """C3's exact product launch: 64 rows x 16 heads x D 128 at T 8192 (the
+    bench's row count and context), 2 layers.  The step's attention is the
+    shipped workgroup-merge form with 8 splits of 65 pages (the split length
+    is derived on device from each row's context: ceil(513 / 8)), the fp32
+    rows quantised by the o_proj prologue -- against the oracle on every row,
+    teacher forced, at the north_star bar."""
+    from oracle.oracle import OracleDecoder
+    rows, T = 64, 8192
+    w, dec = _int8_decoder(oracle, 2, 16, 128, 512, T + 8, rows, seed=53)
+    taps = _Taps(dec, w["cfg"], rows)
+    dec.begin_synthetic(rows, T, 78, True)
+    ns, form = dec.attention_plan()
+    assert (ns, form) == (8, FORM_WG_MERGE), (ns, form)
+    odec = OracleDecoder(oracle, w, rows)
+    decoder_kv_to_oracle(dec, odec, rows, T)
+    flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=3)
+    assert flips < 1e-3 * vals, (flips, vals)
+    print(f"C3 shipped launch: {ns} splits (workgroup merge), attention int8 flips "
+          f"{flips}/{vals}, logits rel err {worst:.2e}")
+
+
+@pytest.mark.timeout(600)
+def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
+    """C5's per-GPU model dims: 32 heads x D 128 (hid 4096, inter 16384), 2
+    layers, 16 rows at T 2048.  hid 4096 keeps the split + pa_merge_row_kernel
+    form (the o_proj quantising prologue takes K <= 2048 only): the merge
+    launch quantises each 4096-wide row into the o_proj's packed int8 A, and
+    the GEMMs run C5's shapes (qkv 4096x12288, o_proj 4096x4096, fc1
+    4096x16384, fc2 16384x4096: 256 k-steps) -- against the oracle, teacher
+    forced at the four int8 GEMM inputs (attention_cpu/cpu_attention_kernel.cpp:103-120,
+    attention_cpu/int8_quant.cpp:5-13, decoder/mlp.hpp:23-41)."""
+    from oracle.oracle import OracleDecoder
+    rows, T = 16, 2048
+    w, dec = _int8_decoder(oracle, 2, 32, 128, 512, T + 8, rows, seed=54)
+    assert w["cfg"]["hid"] == 4096 and w["cfg"]["inter"] == 16384
+    taps = _Taps(dec, w["cfg"], rows)
+    dec.begin_synthetic(rows, T, 79, True)
+    ns, form = dec.attention_plan()
+    assert form == FORM_SPLIT_MERGE_ROW and ns >= 2, (ns, form)
+    odec = OracleDecoder(oracle, w, rows)
+    decoder_kv_to_oracle(dec, odec, rows, T)
+    flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=5)
+    assert flips < 1e-3 * vals, (flips, vals)
+    print(f"C5 dims: {ns} splits (split + merge_row), attention int8 flips {flips}/{vals}, "
+          f"logits rel err {worst:.2e}")
+
+
 def test_int8_c4_beam_state_attention_vs_oracle(gpu, oracle):
     """The C4 bench state (begin_beams(8, 4, 3840, 256): 240 shared tiles per
     sequence through page-table forks, 16 private per beam) at C3 head dims,

@@ -26,6 +26,8 @@ def _dev(a):
     (17, 2048, 2048), (24, 2048, 6144), (32, 8192, 2048), (32, 2048, 8192), (20, 768, 768),
     # 33..64 rows, under 256 column tiles: 2 column tiles x 16-row workgroups
     (33, 2048, 2048), (48, 8192, 2048), (64, 2048, 2048), (40, 768, 2304),
+    # C5's per-GPU shapes (hid 4096, inter 16384): qkv, o_proj, fc1, fc2 (256 k-steps)
+    (64, 4096, 12288), (64, 4096, 4096), (64, 4096, 16384), (64, 16384, 4096),
 ])
 def test_i8_gemm_exact(gpu, oracle, M, K, N):
     import llm_capi
@@ -63,6 +65,9 @@ def test_i8_gemm_no_scales(gpu, oracle):
     (16, 256, 64, 1, 8), (100, 1024, 512, 2, 16), (64, 8192, 2048, 4, 4), (48, 2048, 2048, 4, 8),
     (64, 2048, 6144, 3, 8), (40, 2048, 6144, 3, 8),  # C3's qkv form: 3 column tiles
     (512, 1024, 768, 0, 0), (300, 512, 4096, 0, 0),  # prefill-chunk row counts
+    # C5's per-GPU shapes in the decoder's automatic form (packed A)
+    (64, 4096, 12288, 0, 0), (64, 4096, 4096, 0, 0), (64, 4096, 16384, 0, 0),
+    (64, 16384, 4096, 0, 0),
 ])
 def test_i8_gemm_packed_a_variants_exact(gpu, oracle, M, K, N, nt, waves):
     """The decoder's GEMM form: A in packed-A (MFMA fragment) order, forced

@@ -165,3 +165,109 @@ def test_fused_oproj(gpu, ctx, H, D, ts):
         bound = np.spacing(np.abs(fg).astype(np.float16)).astype(np.float64) + 1e-5 * np.abs(fg).max()
         assert np.all(np.abs(fa - fg) <= bound), np.max(np.abs(fa - fg) / bound)
         assert np.mean(fa != fg) < 0.05, np.mean(fa != fg)
+
+
+def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3):
+    """Fused-o_proj range guard runs (tuning build, forced split count, context
+    0 so each row's attention output is exactly its new V row): per step the
+    logits, llm_decoder_sync's status, then llm_decoder_oproj_status, and the
+    step-0 taps (uint16 [L][4][B16 * qa_ld])."""
+    import torch
+    import llm_capi
+    os.environ["LLM_WGM_SPLITS"] = str(splits)
+    os.environ["LLM_OPROJ_FUSE"] = "1" if fuse else "0"
+    for name, args in (("llm_decoder_create", [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_void_p)]),
+                       ("llm_decoder_set_f16_weights", [ctypes.c_void_p, ctypes.POINTER(_F16W)]),
+                       ("llm_decoder_begin_synthetic", [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                        ctypes.c_uint64, ctypes.c_int]),
+                       ("llm_decoder_step", [ctypes.c_void_p] * 5),
+                       ("llm_decoder_sync", [ctypes.c_void_p]),
+                       ("llm_decoder_set_taps", [ctypes.c_void_p] * 3),
+                       ("llm_decoder_destroy", [ctypes.c_void_p])):
+        getattr(lib, name).argtypes = args
+    lib.llm_decoder_destroy.restype = None
+    cfg = _Cfg(L, H, D, H * D, V, 64, 0, 16, llm_capi.LLM_F16, B, 1.0, 0)
+    dec = ctypes.c_void_p()
+    llm_capi.check(lib.llm_decoder_create(ctypes.byref(cfg), ctypes.byref(dec)), lib)
+    try:
+        ww = _F16W(*[w[k].ctypes.data for k in ("emb", "ln1_g", "ln1_b", "ln2_g", "ln2_b", "wqkv",
+                                                 "wo", "w1", "w2", "b1", "b2")])
+        llm_capi.check(lib.llm_decoder_set_f16_weights(dec, ctypes.byref(ww)), lib)
+        llm_capi.check(lib.llm_decoder_begin_synthetic(dec, B, 0, 77, 1), lib)
+        b16, qa_ld = (B + 15) // 16 * 16, 4 * H * D
+        tq = torch.zeros((L, 4, b16 * qa_ld), dtype=torch.int16, device="cuda")
+        ts_ = torch.zeros((L * 4 * B,), dtype=torch.float32, device="cuda")
+        llm_capi.check(lib.llm_decoder_set_taps(dec, tq.data_ptr(), ts_.data_ptr()), lib)
+        rng = np.random.default_rng(5)
+        logits = torch.empty((B, V), device="cuda")
+        out, rcs, taps = [], [], None
+        for s in range(steps):
+            tok = rng.integers(0, V, B).astype(np.int32)
+            llm_capi.check(lib.llm_decoder_step(dec, tok.ctypes.data, logits.data_ptr(), None, None),
+                           lib)
+            rcs.append(lib.llm_decoder_sync(dec))
+            out.append(logits.cpu().numpy().copy())
+            if s == 0:
+                taps = tq.cpu().numpy().view(np.uint16).copy()
+                llm_capi.check(lib.llm_decoder_set_taps(dec, None, None), lib)
+        clamped, nz = ctypes.c_int(-1), ctypes.c_longlong(-1)
+        llm_capi.check(lib.llm_decoder_oproj_status(dec, ctypes.byref(clamped), ctypes.byref(nz)), lib)
+        return np.stack(out), rcs, (clamped.value, nz.value), taps
+    finally:
+        lib.llm_decoder_destroy(dec)
+        os.environ.pop("LLM_WGM_SPLITS", None)
+        os.environ.pop("LLM_OPROJ_FUSE", None)
+
+
+def test_fused_oproj_range_guard(gpu):
+    """The fused o_proj's counted int64 columns hold |sum| < 2^23 only; each
+    head's term is clamped to (2^23 - 1) / H (common.hpp oacc_term), so the
+    arrival count can never be corrupted, and a clamp raises LLM_ERR_RANGE at
+    llm_decoder_sync.  Layer 0's V projection is made large and its W_o column
+    n0 set to a constant s, so head h of row b adds s * sum(o[b, hD:(h+1)D]):
+    s is chosen from the GEMM form's own tapped o_proj input so that the
+    largest head term is just under the limit (0.97x: the fused form must
+    match the o_proj GEMM, no error) or over it (1.6x: LLM_ERR_RANGE on every
+    step, yet every accumulator column back at zero after each step); a
+    non-finite head (V overflowing fp16) trips it the same way."""
+    import llm_capi
+    from oracle.oracle import unpack_a_f16
+    from _util import rel_err
+    tune = llm_capi.load_tune()
+    L, H, D, V, B = 2, 12, 64, 512, 16
+    hid = H * D
+    rng = np.random.default_rng(11)
+    w = _model(rng, L, H, D, V)
+    w["wqkv"][0, :, 2 * hid:] = rng.standard_normal((hid, hid)).astype(np.float16)
+    n0 = 5
+    w["wo"][0, :, n0] = np.float16(1.0)
+    _, rcs, st, tg = _guard_run(tune, w, L, H, D, V, B, 1, fuse=False)
+    assert rcs == [0] and st == (0, 0), (rcs, st)  # the GEMM form has no accumulator
+    o = unpack_a_f16(tg[0, 1], B, hid).astype(np.float32)  # layer 0's o_proj input
+    head_sums = o.reshape(B, H, D).sum(axis=2)
+    lim = ((1 << 23) - 1) / H
+    peak = float(np.abs(head_sums).max())
+    for frac, trips in ((0.97, False), (1.6, True)):
+        s = np.float16(frac * lim / peak)
+        assert np.isfinite(s) and s > 0
+        ws = dict(w)
+        ws["wo"] = w["wo"].copy()
+        ws["wo"][0, :, n0] = s
+        ws = {k: np.ascontiguousarray(v) for k, v in ws.items()}
+        gl, grc, gst, gt = _guard_run(tune, ws, L, H, D, V, B, 2, fuse=False)
+        fl, frc, fst, ft = _guard_run(tune, ws, L, H, D, V, B, 2, fuse=True)
+        assert grc == [0, 0] and gst == (0, 0)
+        assert fst[1] == 0, fst  # every column completed and cleared
+        if not trips:
+            assert frc == [0, 0] and fst == (0, 0), (frac, frc, fst)
+            assert rel_err(fl[0], gl[0]) < 1e-3, rel_err(fl[0], gl[0])
+            assert np.array_equal(ft[0, 1], gt[0, 1])  # same o_proj input
+        else:
+            assert frc == [llm_capi.LLM_ERR_RANGE] * 2 and fst == (1, 0), (frc, fst)
+    # non-finite heads: V rows overflow fp16 (inf), the merged heads are inf / NaN
+    wn = dict(w)
+    wn["wqkv"] = w["wqkv"].copy()
+    wn["wqkv"][0, :, 2 * hid:] = (3000 * rng.standard_normal((hid, hid))).astype(np.float16)
+    wn = {k: np.ascontiguousarray(v) for k, v in wn.items()}
+    _, frc, fst, _ = _guard_run(tune, wn, L, H, D, V, B, 2, fuse=True)
+    assert frc == [llm_capi.LLM_ERR_RANGE] * 2 and fst == (1, 0), (frc, fst)
