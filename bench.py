@@ -228,6 +228,13 @@ def cpu_baseline(cfg_name, budget_s=20.0):
     res["cpus_available"] = avail
     res["cpu"]["cpus_available"] = avail  # (the child's own affinity is one place once bound)
     res["omp"] = {"OMP_NUM_THREADS": threads, "OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}
+    env_omp = os.environ.get("OMP_NUM_THREADS", "")
+    res["threads_reason"] = (
+        f"the job's OpenMP share: OMP_NUM_THREADS={env_omp} set by the GPU pool for a 1-GPU job "
+        f"on a host shared by 8 GPUs' jobs ({avail} CPUs in the affinity mask); BASELINE.md asks "
+        f"for $(nproc), which here would take the other jobs' CPUs"
+        if env_omp.isdigit() and int(env_omp) > 0 and int(env_omp) < avail
+        else f"every CPU in this process's affinity mask ({avail})")
     return res
 
 
@@ -453,7 +460,8 @@ def main():
                                                       f"over {world} GPU(s)" if strong else ""),
                        "global_batch": args.global_batch if strong else B * world,
                        "batch_per_gpu": B, "seq_len": T, "page_size": cfg["ts"],
-                       "parallelism": f"batch-sharded x{world} (RCCL {args.gather} gather to rank 0)"
+                       "parallelism": "single GPU (no collective)" if world == 1
+                       else f"batch-sharded x{world} (RCCL {args.gather} gather to rank 0)"
                        if not host_gather else f"batch-sharded x{world} ({backend} rehearsal)"},
             "hbm_roofline_frac_step": round(step_b / t_step / 1e9 / HBM_PEAK_GBPS, 4),
             "step_bytes": int(step_b),

@@ -227,8 +227,8 @@ def test_fused_oproj_range_guard(gpu):
     n0 set to a constant s, so head h of row b adds s * sum(o[b, hD:(h+1)D]):
     s is chosen from the GEMM form's own tapped o_proj input so that the
     largest head term is just under the limit (0.97x: the fused form must
-    match the o_proj GEMM, no error) or over it (1.6x: LLM_ERR_RANGE on every
-    step, yet every accumulator column back at zero after each step); a
+    match the o_proj GEMM, no error; one step) or over it (1.6x: LLM_ERR_RANGE
+    on both steps, yet every accumulator column back at zero); a
     non-finite head (V overflowing fp16) trips it the same way."""
     import llm_capi
     from oracle.oracle import unpack_a_f16
@@ -254,12 +254,15 @@ def test_fused_oproj_range_guard(gpu):
         ws["wo"] = w["wo"].copy()
         ws["wo"][0, :, n0] = s
         ws = {k: np.ascontiguousarray(v) for k, v in ws.items()}
-        gl, grc, gst, gt = _guard_run(tune, ws, L, H, D, V, B, 2, fuse=False)
-        fl, frc, fst, ft = _guard_run(tune, ws, L, H, D, V, B, 2, fuse=True)
-        assert grc == [0, 0] and gst == (0, 0)
+        # (one step just under: the step-0 heads set s; the next step's heads
+        # attend two V rows and may be larger)
+        steps = 2 if trips else 1
+        gl, grc, gst, gt = _guard_run(tune, ws, L, H, D, V, B, steps, fuse=False)
+        fl, frc, fst, ft = _guard_run(tune, ws, L, H, D, V, B, steps, fuse=True)
+        assert grc == [0] * steps and gst == (0, 0)
         assert fst[1] == 0, fst  # every column completed and cleared
         if not trips:
-            assert frc == [0, 0] and fst == (0, 0), (frac, frc, fst)
+            assert frc == [0] and fst == (0, 0), (frac, frc, fst)
             assert rel_err(fl[0], gl[0]) < 1e-3, rel_err(fl[0], gl[0])
             assert np.array_equal(ft[0, 1], gt[0, 1])  # same o_proj input
         else:
