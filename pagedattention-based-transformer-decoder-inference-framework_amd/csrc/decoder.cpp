@@ -76,6 +76,9 @@ struct llm_decoder {
   // FP16: W_o again as per-head column slices for the fused o_proj,
   // [L][H][D/8][hid][8] (PaRowOutputs::wo_heads)
   DevBuf<uint16_t> wo_heads;
+  // FP16: W_qkv again as per-head column slices for the fused LN1 + q/k/v
+  // projection, [L][H][hid/8][3D][8] (PaRowOutputs::qkv_w)
+  DevBuf<uint16_t> wqkv_heads;
   size_t sz_qkv = 0, sz_o = 0, sz_1 = 0, sz_2 = 0;
   bool weights_ready = false;
   int w_keep = 0;  // the GEMM weights fit the Infinity Cache: keep them there (w_keep_for)
@@ -89,6 +92,12 @@ struct llm_decoder {
   DevBuf<int32_t> lm_pi;
   int lm_nwg = 0;
   DevBuf<int8_t> qa;
+  // INT8 decode rows: the LayerNorm outputs the o_proj / fc2 last-arriver
+  // seam writes (GemmArgs::lnx_*), packed int8 [B16][hid] + row scales, and
+  // its arrival counters (one per 16-row block, zero between launches)
+  DevBuf<int8_t> qa_ln;
+  DevBuf<float> sa_ln;
+  DevBuf<unsigned> lnx_cnt;
   DevBuf<uint16_t> a16;
   // FP16: the fused o_proj's int64 columns [max_batch][hid] (zero between
   // attention launches: the adder completing a column clears it); oacc_run:
@@ -117,6 +126,7 @@ struct llm_decoder {
   int layer_norm_into(WeightGemm& g, const struct Rows& R, const float* gamma, const float* beta,
                       hipStream_t st);
   LnSource embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
+  LnSource attn_src;   // fused q/k/v: layer 0's attention reads E[token] rows itself
 
   ~llm_decoder() {
     if (h_oflag) (void)hipHostFree(h_oflag);
@@ -140,6 +150,7 @@ struct llm_decoder {
   int layer_attn(int l, hipStream_t st, const struct Rows& R, PaPlan* plan = nullptr);
   bool quant_prologue(const struct Rows& R) const;
   bool oproj_fusable(const struct Rows& R);
+  void fuse_decode_rows(struct Rows& R, float* oproj_out, long long* acc);
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -203,6 +214,12 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->sa.alloc((size_t)B));
   const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
   RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
+  if (d->wdtype == LLM_I8) {
+    RET_IF(d->qa_ln.alloc(B16 * hid));
+    RET_IF(d->sa_ln.alloc((size_t)B));
+    RET_IF(d->lnx_cnt.alloc(B16 / 16));
+    LLM_HIP_RET(hipMemset(d->lnx_cnt.p, 0, sizeof(unsigned) * d->lnx_cnt.n));
+  }
   if (d->wdtype == LLM_F16) {
     RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
     RET_IF(d->oacc.alloc((size_t)B * hid));
@@ -355,6 +372,28 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
                             sizeof(uint16_t) * hid * hid, hipMemcpyHostToDevice));
     }
   }
+  // the fused q/k/v projection's head slices: [h][kg][c][j] = W_qkv[8 kg + j][col(h, c)],
+  // c < D the head's q columns, then its k and its v columns (a second copy of
+  // W_qkv, L * 3 hid^2 fp16, only where the fused form can run)
+  d->wqkv_heads.alloc(0);
+  if (d->wo_heads.p && hid <= 2048 && qkv_fuse_on()) {
+    const int D = d->D, KG = hid / 8, NC = 3 * D;
+    const uint16_t* src = static_cast<const uint16_t*>(w->wqkv);
+    std::vector<uint16_t> sl((size_t)hid * 3 * hid);
+    RET_IF(d->wqkv_heads.alloc((size_t)L * hid * 3 * hid));
+    for (int l = 0; l < L; ++l) {
+      const uint16_t* wl = src + (size_t)l * hid * 3 * hid;
+      for (int h = 0; h < d->H; ++h)
+        for (int kg = 0; kg < KG; ++kg)
+          for (int c = 0; c < NC; ++c) {
+            const size_t n = (size_t)(c / D) * hid + (size_t)h * D + c % D;
+            for (int j = 0; j < 8; ++j)
+              sl[(((size_t)h * KG + kg) * NC + c) * 8 + j] = wl[(size_t)(8 * kg + j) * 3 * hid + n];
+          }
+      LLM_HIP_RET(hipMemcpy(d->wqkv_heads.p + (size_t)l * hid * 3 * hid, sl.data(),
+                            sizeof(uint16_t) * hid * 3 * hid, hipMemcpyHostToDevice));
+    }
+  }
   RET_IF(upload_packed(d->w1, d->sz_1, w->w1, L, hid, inter, LLM_F16, "w1"));
   RET_IF(upload_packed(d->w2, d->sz_2, w->w2, L, inter, hid, LLM_F16, "w2"));
   RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
@@ -380,6 +419,12 @@ struct Rows {
   void* act = nullptr;  // packed-A GEMM input (int8 or fp16), 16-row tiles
   void* act2 = nullptr; // fp16 decoder: fc2's packed input (written by fc1 while act is read)
   float* sa = nullptr;  // [n] int8 row scales
+  // INT8 decode rows, LayerNorm seam (ln_seam): LN2 (after o_proj) and the
+  // next layer's LN1 (after fc2) are computed by those GEMMs' last-arriving
+  // workgroups into act_ln / sa_ln, which fc1 and the next qkv read
+  bool ln_seam = false;
+  void* act_ln = nullptr;
+  float* sa_ln = nullptr;
   const int32_t* pos = nullptr;  // [n] position written this pass
   const int32_t* ctx = nullptr;  // [n] context length attended (pos + 1)
   const int32_t* beam_rows = nullptr;  // page-table row per row; NULL: table_row0 + m
@@ -396,6 +441,9 @@ struct Rows {
   // scratch row for llm_decoder_run_attention); no o_proj launch
   long long* oacc = nullptr;
   float* oproj_out = nullptr;
+  // ... and, with it, LN1 + the q/k/v projection + the KV append (qkv_fused):
+  // no q/k/v GEMM launch; the step's first attention reads E[token] rows
+  bool qkv_fused = false;
 };
 
 // Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
@@ -406,6 +454,11 @@ struct Rows {
 // elements).
 int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   const size_t lh = (size_t)l * hid;
+  if (R.qkv_fused) {  // the attention's workgroups normalise and project their rows themselves
+    attn_src = embed_src;
+    embed_src = LnSource{};
+    return LLM_OK;
+  }
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
   KvAppendView app;
@@ -431,7 +484,12 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   g.C = R.q; g.c_cols = hid; g.c_ld = hid;  // q only: K and V go straight into the pages
   g.kv = &app;
   if (wdtype == LLM_I8) g.sa = R.sa, g.sw = sw_qkv.p + (size_t)l * 3 * hid;
-  RET_IF(layer_norm_into(g, R, ln1_g.p + lh, ln1_b.p + lh, st));
+  if (R.ln_seam && l > 0) {  // LN1 was written by the previous layer's fc2 (seam)
+    g.A = R.act_ln;
+    g.sa = R.sa_ln;
+  } else {
+    RET_IF(layer_norm_into(g, R, ln1_g.p + lh, ln1_b.p + lh, st));
+  }
   RET_IF(weight_gemm(g, st));
   return tap(l, 0, R, hid, st);
 }
@@ -483,9 +541,20 @@ bool llm_decoder::oproj_fusable(const Rows& R) {
   Rows r = R;
   r.oacc = oacc.p;
   r.oproj_out = R.x;
+  r.qkv_fused = false;
   PaPlan p;
   if (layer_attn(0, stream, r, &p) != LLM_OK) return false;
   return (p.form & LLM_PA_FORM_OPROJ) != 0;
+}
+
+// Decode rows whose o_proj runs in the attention's workgroup merge (into the
+// columns acc, writing oproj_out) and, where the per-head W_qkv slices exist,
+// whose LN1 + q/k/v projection + KV append run in the same workgroups.
+void llm_decoder::fuse_decode_rows(Rows& R, float* oproj_out, long long* acc) {
+  if (!oproj_fusable(R)) return;
+  R.oacc = acc;
+  R.oproj_out = oproj_out;
+  R.qkv_fused = wqkv_heads.p != nullptr;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
@@ -524,13 +593,30 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
     ro.wo_heads = wo_heads.p + (size_t)l * hid * hid;
     ro.o_n = hid;
     ro.o_flag = oflag.p;
+    if (R.qkv_fused) {
+      ro.qkv_w = wqkv_heads.p + (size_t)l * hid * 3 * hid;
+      ro.ln_x = R.x;
+      if (attn_src.emb) {
+        ro.ln_emb = attn_src.emb;
+        ro.ln_tok = attn_src.tok;
+        ro.ln_V = attn_src.V;
+      }
+      if (!plan) attn_src = LnSource{};
+      ro.ln_g = ln1_g.p + (size_t)l * hid;
+      ro.ln_b = ln1_b.p + (size_t)l * hid;
+      ro.ln_eps = 1e-5f;
+      ro.ln_tap = tap_q ? R.act2 : nullptr;  // (R.act takes the attention rows)
+    }
     ro.out16 = tap_q ? R.act : nullptr;  // the taps read the packed o_proj input
   } else {
     ro.out16 = R.act;
   }
-  return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
+  RET_IF(pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
-                            R.row_group, plan);
+                            R.row_group, plan));
+  // the fused form wrote the LN1 rows (the q/k/v GEMM's A) for the taps
+  if (R.qkv_fused && !plan) RET_IF(tap(l, 0, R, hid, st));
+  return LLM_OK;
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
@@ -552,11 +638,21 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
     g.ln_quant_only = 1;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
   }
+  if (R.ln_seam) {  // LN2 by o_proj's last-arriving workgroups
+    g.lnx_g = ln2_g.p + lh; g.lnx_b = ln2_b.p + lh;
+    g.lnx_act = R.act_ln; g.lnx_sa = R.sa_ln; g.lnx_cnt = lnx_cnt.p;
+  }
   if (!R.oacc) RET_IF(weight_gemm(g, st));  // (fused: the attention wrote x)
   g.ln_x = nullptr; g.ln_quant_only = 0; g.act_out = nullptr; g.sa_out = nullptr;
+  g.lnx_cnt = nullptr;
   RET_IF(tap(l, 1, R, hid, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
-  RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
+  if (R.ln_seam) {
+    g.A = R.act_ln;
+    g.sa = R.sa_ln;
+  } else {
+    RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
+  }
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
   if (i8) {
@@ -572,7 +668,8 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   RET_IF(tap(l, 2, R, hid, st));
   g.ln_x = nullptr; g.ln_emb = nullptr; g.act_out = nullptr; g.sa_out = nullptr;
   g.C16 = nullptr;
-  if (!i8) g.A = R.act2;
+  g.A = i8 ? R.act : R.act2;
+  g.sa = R.sa;
   // quantise h1 -> mlp_fc2 (+b2)
   if (i8)
     LLM_HIP_RET(launch_quantize_rows(R.h1, R.n, inter, static_cast<int8_t*>(R.act), R.sa, st, 1));
@@ -580,6 +677,11 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
+  if (R.ln_seam && l + 1 < L) {  // the next layer's LN1 by fc2's last-arriving workgroups
+    const size_t ln = (size_t)(l + 1) * hid;
+    g.lnx_g = ln1_g.p + ln; g.lnx_b = ln1_b.p + ln;
+    g.lnx_act = R.act_ln; g.lnx_sa = R.sa_ln; g.lnx_cnt = lnx_cnt.p;
+  }
   return weight_gemm(g, st);
 }
 
@@ -594,6 +696,12 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
   R.act = wdtype == LLM_I8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
   if (wdtype == LLM_F16) R.act2 = a16.p + (b16 + (size_t)r0) * qa_ld;
   R.sa = sa.p + r0;
+  if (wdtype == LLM_I8 && lnx_on() && !ln_fusable(wdtype, n, hid) && lnx_ok(wdtype, n, hid) &&
+      lnx_cnt.p) {
+    R.ln_seam = true;
+    R.act_ln = qa_ln.p + (size_t)r0 * hid;
+    R.sa_ln = sa_ln.p + r0;
+  }
   R.pos = pos.p + r0;
   R.ctx = ctx.p + r0;
   R.table_row0 = r0;
@@ -615,11 +723,12 @@ int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
   const size_t slot = (size_t)l * 4 + stage;
   const size_t n16 = ((size_t)R.n + 15) / 16 * 16;
   const size_t r0 = (size_t)R.table_row0;  // rows r0.. of the step (16-row aligned)
-  const void* src = f16 && stage == 3 ? R.act2 : R.act;
+  const bool seam = R.ln_seam && (stage == 2 || (stage == 0 && l > 0));  // LN written by a seam
+  const void* src = seam ? R.act_ln : f16 && (stage == 3 || (stage == 0 && R.qkv_fused)) ? R.act2 : R.act;
   LLM_HIP_RET(hipMemcpyAsync(tap_q + (slot * b16 * qa_ld + r0 * K) * es, src, n16 * K * es,
                              hipMemcpyDeviceToDevice, st));
   if (!f16)
-    LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, R.sa, sizeof(float) * R.n,
+    LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, seam ? R.sa_ln : R.sa, sizeof(float) * R.n,
                                hipMemcpyDeviceToDevice, st));
   return LLM_OK;
 }
@@ -665,7 +774,7 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
 // One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
   Rows R = step_rows(0, batch, attn_ws.p);
-  if (oproj_fusable(R)) R.oacc = oacc.p, R.oproj_out = R.x;
+  fuse_decode_rows(R, R.x, oacc.p);
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -836,6 +945,7 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
   if (d->oacc.p) LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * d->oacc.n));
   if (d->oflag.p) LLM_HIP_RET(hipMemset(d->oflag.p, 0, sizeof(int)));
+  if (d->lnx_cnt.p) LLM_HIP_RET(hipMemset(d->lnx_cnt.p, 0, sizeof(unsigned) * d->lnx_cnt.n));
   std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
   LLM_HIP_RET(hipMemcpy(d->pos.p, pos.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
   LLM_HIP_RET(hipMemcpy(d->ctx.p, ctx.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
@@ -946,7 +1056,7 @@ extern "C" int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form
   std::lock_guard<std::mutex> g(d->mu);
   LLM_REQUIRE(d->batch > 0, "llm_decoder_attention_plan: no active rows");
   Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
-  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.x;
+  d->fuse_decode_rows(R, R.x, d->oacc.p);
   PaPlan p;
   RET_IF(d->layer_attn(0, d->stream, R, &p));
   *nsplit = p.nsplit;
@@ -969,7 +1079,16 @@ extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream
       RET_IF(d->oacc_run.alloc(d->oacc.n));
       LLM_HIP_RET(hipMemset(d->oacc_run.p, 0, sizeof(long long) * d->oacc_run.n));
     }
-    R.oacc = d->oacc_run.p, R.oproj_out = R.o;
+    d->fuse_decode_rows(R, R.o, d->oacc_run.p);
+    // the fused q/k/v form normalises x (layer 0: the next tokens' embedding
+    // rows) and appends k, v at each row's next position, which the next step
+    // overwrites
+    if (R.qkv_fused && layer == 0) {
+      d->attn_src = LnSource{};
+      d->attn_src.emb = reinterpret_cast<const _Float16*>(d->emb.p);
+      d->attn_src.tok = d->tokens.p;
+      d->attn_src.V = d->V;
+    }
   }
   return d->layer_attn(layer, st, R);
 }

@@ -13,5 +13,8 @@ hipError_t tune_launch_beam4(const PaSplitArgs& a, int D, int TS, hipStream_t st
 // pa_beam_mfma_kernel (D 128, page 16) on pa_split_kernel's BEAM grid
 hipError_t tune_launch_beam_mfma(const PaSplitArgs& a, dim3 grid, hipStream_t st);
 hipError_t tune_beam_mfma_occupancy(int* blocks);
+// the shipped BEAM form of pa_split_kernel (D 128, page 16) with a trivial
+// consumer (LOAD_ONLY): its loads, LDS staging and barriers without the maths
+hipError_t tune_launch_beam_loads_only(const PaSplitArgs& a, dim3 grid, hipStream_t st);
 
 }  // namespace llm

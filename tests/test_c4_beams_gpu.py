@@ -95,8 +95,9 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     empty splits, ragged contexts, beam_ids routing inside a group, a missing
     shared page, and never-written (NaN) token rows past every context in both
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
-    cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1)
-    and its one-wave-per-group kernel (LLM_BEAM4=1)."""
+    cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1),
+    its one-wave-per-group kernel (LLM_BEAM4=1) and that schedule with MFMA
+    q.k (LLM_BEAM4=2)."""
     import torch
     import llm_capi
     rng = np.random.default_rng(B * 7 + T)
@@ -170,3 +171,12 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     assert np.isfinite(out4).all()
     assert_parity(out4, ref, 1e-3)
     assert rel_err(out4, plain) < 1e-5
+    # ... and the same schedule with the 4 beams' q.k on the matrix cores
+    # (pa_beam_mq_kernel, LLM_BEAM4=2; D 128, page 16)
+    monkeypatch.setenv("LLM_BEAM4", "2")
+    outq = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                              beam_ids=d(beam_ids), row_group=4,
+                              lib=llm_capi.load_tune()).cpu().numpy()
+    assert np.isfinite(outq).all()
+    assert_parity(outq, ref, 1e-3)
+    assert rel_err(outq, plain) < 1e-5
