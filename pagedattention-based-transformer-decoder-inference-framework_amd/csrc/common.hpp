@@ -1,6 +1,10 @@
 // Shared host/device helpers for the gfx950 decode path.
 #pragma once
 
+#ifndef LLM_TUNING
+#define LLM_TUNING 0  // 1: the tuning library (Makefile `tune`)
+#endif
+
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

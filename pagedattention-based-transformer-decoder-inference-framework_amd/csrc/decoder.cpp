@@ -214,7 +214,7 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->sa.alloc((size_t)B));
   const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
   RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
-  if (d->wdtype == LLM_I8) {
+  if (d->wdtype == LLM_I8 && lnx_on()) {  // the LayerNorm seam (tuning build)
     RET_IF(d->qa_ln.alloc(B16 * hid));
     RET_IF(d->sa_ln.alloc((size_t)B));
     RET_IF(d->lnx_cnt.alloc(B16 / 16));
@@ -696,8 +696,8 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
   R.act = wdtype == LLM_I8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
   if (wdtype == LLM_F16) R.act2 = a16.p + (b16 + (size_t)r0) * qa_ld;
   R.sa = sa.p + r0;
-  if (wdtype == LLM_I8 && lnx_on() && !ln_fusable(wdtype, n, hid) && lnx_ok(wdtype, n, hid) &&
-      lnx_cnt.p) {
+  if (wdtype == LLM_I8 && lnx_on() && !ln_fusable(wdtype, n, hid) && lnx_ok(wdtype, n, hid, hid) &&
+      lnx_ok(wdtype, n, hid, inter) && lnx_cnt.p) {  // (o_proj and fc2)
     R.ln_seam = true;
     R.act_ln = qa_ln.p + (size_t)r0 * hid;
     R.sa_ln = sa_ln.p + r0;

@@ -80,9 +80,10 @@ struct LnSource {
 };
 
 int weight_gemm(const WeightGemm& g, hipStream_t st);
-// Whether an I8 weight GEMM of M rows and N output columns can end in the
-// last-arriver LayerNorm seam (WeightGemm::lnx_*): N <= 2048, N % 64 == 0.
-bool lnx_ok(int dtype, int M, int N);
+// Whether an I8 weight GEMM of M rows, N output columns and K inputs can end
+// in the last-arriver LayerNorm seam (WeightGemm::lnx_*): N <= 2048, N % 64 ==
+// 0, and the launch tiles the rows 16 per workgroup.
+bool lnx_ok(int dtype, int M, int N, int K);
 // Whether the LNX seam is switched on (tuning build: LLM_LNX=0 switches it off).
 bool lnx_on();
 // Whether weight_gemm can run the LayerNorm prologue for M rows of K (the

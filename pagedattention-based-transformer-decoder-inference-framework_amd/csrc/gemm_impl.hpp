@@ -707,18 +707,21 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t
   if constexpr (NT <= 2) {
     if (a.ln_x) {
       const size_t lds = ln_lds_bytes<KIND, MT, NT, 8>(a.K);
+#if LLM_TUNING
       if constexpr (KIND == GemmKind::I8) {
-        if (a.lnx_cnt) {  // + the last-arriver LayerNorm seam
+        if (a.lnx_cnt) {  // + the last-arriver LayerNorm seam (tuning build)
           hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1, 1>), grid, dim3(512), lds, st, a);
           return hipGetLastError();
         }
       }
+#endif
       hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1>), grid, dim3(512), lds, st, a);
       return hipGetLastError();
     }
   }
+#if LLM_TUNING
   if constexpr (KIND == GemmKind::I8 && NT <= 2) {
-    if (a.lnx_cnt) {  // the last-arriver LayerNorm seam (no split-K: lnx_ok)
+    if (a.lnx_cnt) {  // the last-arriver LayerNorm seam (tuning build; no split-K: lnx_ok)
       if constexpr (MT * NT * 8 <= 64) {
         if (waves != 4) {
           hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 0, 1>), grid, dim3(512), 0, st, a);
@@ -729,6 +732,7 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t
       return hipGetLastError();
     }
   }
+#endif
   // the cross-wave sums' static LDS (WAVES x MT NT KiB) must stay <= 64 KiB
   if constexpr (MT * NT * 8 <= 64) {
     if (waves != 4) {

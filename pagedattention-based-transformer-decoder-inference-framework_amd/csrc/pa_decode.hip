@@ -310,13 +310,13 @@ bool oproj_fuse_on() {
 #endif
 }
 // The FP16 decoder's LayerNorm + q/k/v projection + KV append fused into the
-// same workgroups (decoder.cpp qkv_fusable); the tuning build's
-// LLM_QKV_FUSE=0 restores the q/k/v GEMM launch (A/B, parity).
+// same workgroups (decoder.cpp): tuning build only (LLM_QKV_FUSE=1), since
+// same-box it lost C2 -6.6 % against the q/k/v GEMM launch.
 bool qkv_fuse_on() {
 #if LLM_TUNING
-  return env_int("LLM_QKV_FUSE", 1) != 0;
+  return env_int("LLM_QKV_FUSE", 0) != 0;
 #else
-  return true;
+  return false;
 #endif
 }
 namespace {
@@ -347,6 +347,7 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
   constexpr int ST = split_stages<D, TS, LLM_F16>();
   if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct
     if constexpr (D <= kOprojMaxD) {
+#if LLM_TUNING
       if (a.o_acc && a.qkv_w) {  // + the fused LayerNorm / q, k, v projection / KV append
         if (a.H * D <= 1024)
           hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
@@ -358,6 +359,7 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
                              dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
         return hipGetLastError();
       }
+#endif
       if (a.o_acc) {
         hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
                                             LLM_F16, true, true, true>),
@@ -397,6 +399,11 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
       if (env_int("LLM_BEAM_DIAG", 0) == 1) {  // this form's loads, staging and barriers only
         *beam = true;
         return tune_launch_beam_loads_only(a, grid, st);
+      }
+      const int ring = env_int("LLM_BEAM_RING", 0);
+      if (ring > 0) {  // shared chunks through an LDS-DMA ring
+        *beam = true;
+        return tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
       }
     }
 #endif
@@ -672,6 +679,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
               "head_dim <= 128 and at most 64 heads");
   // + the fused LayerNorm / q, k, v projection (PaRowOutputs::qkv_w)
   const bool qkv = oproj && rows->qkv_w;
+  LLM_REQUIRE(!qkv || LLM_TUNING, "pa_decode: the fused q/k/v projection is a tuning-build form");
   LLM_REQUIRE(!qkv || ((rows->ln_x || (rows->ln_emb && rows->ln_tok && rows->ln_V > 0)) &&
                        rows->ln_g && rows->ln_b && (H * D) % 8 == 0 && H * D <= kQkvMaxHid &&
                        context_lens),

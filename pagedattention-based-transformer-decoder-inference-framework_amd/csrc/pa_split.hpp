@@ -281,7 +281,7 @@ __device__ __forceinline__ void qkv_prologue(const PaSplitArgs& a, int b, int h,
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int QKV = 0>
+          int QKV = 0, int RING = 0>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -576,8 +576,9 @@ void pa_split_kernel(PaSplitArgs a) {
   if constexpr (BEAM) {
     static_assert(NR % 2 == 0, "beam prefetch splits a chunk's 2*NR pieces in quarters");
     constexpr int QP = NR / 2;  // pieces per wave per chunk
+    static_assert(RING == 0 || (RING >= 3 && (RING - 2) * QP < 64), "ring of 3+ chunks");
     __shared__ int pid_lds[4][128];
-    __shared__ __attribute__((aligned(16))) u32x4 kvbuf[2][2 * NR][64];
+    __shared__ __attribute__((aligned(16))) u32x4 kvbuf[RING > 0 ? RING : 2][2 * NR][64];
     if (share) {
       pid_lds[gi][lane] = pid0;
       pid_lds[gi][64 + lane] = pid1;
@@ -616,7 +617,67 @@ void pa_split_kernel(PaSplitArgs a) {
           qr[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + i * 1024, 0, AUX);
         }
       };
-      if (nsh > 0) {
+      if constexpr (RING > 0) {
+        // LDS-DMA ring (tuning): each wave's quarter of chunk cc goes straight
+        // from HBM into ring slot cc % RING (buffer_load ... lds: lane-linear,
+        // no VGPR stage, no ds_write pass), RING - 1 chunks in flight per
+        // workgroup.  Per chunk: the wave's own pieces of cc are retired by a
+        // counted vmcnt (the later chunks stay in flight), one raw barrier
+        // publishes every wave's pieces and retires the reads of slot
+        // (cc - 1) % RING, which the next DMA then refills.  Chunks past the
+        // shared prefix are issued with zero records (no bytes, no fault) so
+        // every wait counts the same number of loads.
+        if (nsh > 0) {
+          auto dma = [&](int cc) {
+            const int slot = cc % RING;
+#pragma unroll
+            for (int t = 0; t < QP; ++t) {
+              const int q = gi * QP + t;
+              const int pi = q % NR;
+              const int u = pi / NI, i = pi % NI;
+              const int j = cc * U + u;
+              const int pg = page_of(min(j, kMaxPps - 1));
+              const bool ok = cc < nsh && j < count && pg >= 0;
+              const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
+              const uint8_t* pool = q < NR ? a.k_pool : a.v_pool;
+              const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pool + off), (short)0,
+                                                                ok ? PAGE_BYTES : 0, 0x00020000);
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  rs, (__attribute__((address_space(3))) void*)&kvbuf[slot][q][0], 16,
+                  lane_off + i * 1024, 0, 0, AUX);
+            }
+          };
+#pragma unroll
+          for (int c0 = 0; c0 < RING - 1; ++c0) dma(c0);
+          for (int cc = 0; cc < nsh; ++cc) {
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((RING - 2) * QP)
+                         : "memory");
+            const int cur = cc % RING;
+            u32x4 kk[NR], vv[NR];
+            // the slot's reads as one asm block (+ lgkmcnt(0)): read through
+            // plain LDS loads, the compiler would retire every DMA in flight
+            // (vmcnt(0)) before them, which is the ring's whole point lost
+            const uint32_t ra = (uint32_t)(size_t)(
+                __attribute__((address_space(3))) void*)&kvbuf[cur][0][lane];
+            static_assert(NR == 4, "the ring's asm reads are written for 8 KiB chunks");
+            asm volatile(
+                "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:1024\n\t"
+                "ds_read_b128 %2, %8 offset:2048\n\tds_read_b128 %3, %8 offset:3072\n\t"
+                "ds_read_b128 %4, %8 offset:4096\n\tds_read_b128 %5, %8 offset:5120\n\t"
+                "ds_read_b128 %6, %8 offset:6144\n\tds_read_b128 %7, %8 offset:7168\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&v"(kk[0]), "=&v"(kk[1]), "=&v"(kk[2]), "=&v"(kk[3]), "=&v"(vv[0]), "=&v"(vv[1]),
+                  "=&v"(vv[2]), "=&v"(vv[3])
+                : "v"(ra)
+                : "memory");
+            dma(cc + RING - 1);
+            compute(kk, vv, cc * U);
+          }
+          // the zero-record tail loads write LDS the ring no longer reads;
+          // retire them before the direct path's own loads are counted
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else if (nsh > 0) {
         u32x4 qr[QP];
         quarter(qr, 0);
 #pragma unroll

@@ -683,8 +683,10 @@ __global__ __launch_bounds__(256) void pa_beam_mfma_kernel(PaSplitArgs a) {
 // p.v on VALU (one fma per element and beam, V in its natural layout: lane L
 // holds token 4 i + (L >> 4), dims 8 (L & 15) .. + 7).  The VALU form spends
 // 4 waves x ~120 instructions per shared page; this form ~180 for all 4.
-// D 128, page 16, fp16 only.
-template <int MINW = 2>
+// D 128, page 16, fp16 only.  STAGES: pages in flight per wave (2: the next
+// page loads while the current one is computed; 1: latency hidden by the
+// third wave per SIMD the freed registers allow, MINW 3).
+template <int MINW = 2, int STAGES = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void pa_beam_mq_kernel(PaSplitArgs a) {
   constexpr int D = 128, TS = 16, G = 4;
   constexpr int PAGE_BYTES = TS * D * 2;
@@ -761,20 +763,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
           const int t = 64 * k + lane;
           idv[k][i] = t < ntiles ? a.page_table[prow_off[i] + t] : -1;
         }
-      int blk = 0;
-      for (; blk < min(ntiles, 512); blk += 64) {
-        const int k = blk >> 6;
-        const int t = blk + lane;
-        bool eq = t < ntiles;
+      bool done = false;
 #pragma unroll
-        for (int i = 1; i < G; ++i) eq = eq && idv[k][i] == idv[k][0];
-        const uint64_t mk = __ballot(eq);
-        const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
-        nsh = blk + run;
-        if (run < 64) break;
+      for (int k = 0; k < 8; ++k) {  // (k static: idv stays in registers)
+        const int t = 64 * k + lane;
+        if (!done && 64 * k < ntiles) {
+          bool eq = t < ntiles;
+#pragma unroll
+          for (int i = 1; i < G; ++i) eq = eq && idv[k][i] == idv[k][0];
+          const uint64_t mk = __ballot(eq);
+          const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
+          nsh = 64 * k + run;
+          done = run < 64;
+        }
       }
       if (nsh >= 512) {
-        for (blk = 512; blk < ntiles; blk += 64) {
+        for (int blk = 512; blk < ntiles; blk += 64) {
           const int t = blk + lane;
           bool eq = t < ntiles;
           if (eq) {
@@ -895,14 +899,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
           }
       }
     };
-    u32x4 kA[4], vA[4], kB[4], vB[4];
-    issue(kA, vA, 0);
-    for (int j = 0; j < cnt; j += 2) {
-      issue(kB, vB, j + 1);
-      compute(kA, vA, j);
-      if (j + 1 >= cnt) break;
-      issue(kA, vA, j + 2);
-      compute(kB, vB, j + 1);
+    if constexpr (STAGES == 1) {
+      u32x4 kA[4], vA[4];
+      for (int j = 0; j < cnt; ++j) {
+        issue(kA, vA, j);
+        compute(kA, vA, j);
+      }
+    } else {
+      u32x4 kA[4], vA[4], kB[4], vB[4];
+      issue(kA, vA, 0);
+      for (int j = 0; j < cnt; j += 2) {
+        issue(kB, vB, j + 1);
+        compute(kA, vA, j);
+        if (j + 1 >= cnt) break;
+        issue(kA, vA, j + 2);
+        compute(kB, vB, j + 1);
+      }
     }
   }
 
@@ -928,9 +940,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) voi
   }
 }
 
-#ifndef BEAM_MQ_MINW
-#define BEAM_MQ_MINW 2
-#endif
 #ifndef BEAM4_MINW
 #define BEAM4_MINW 2
 #endif
@@ -962,13 +971,15 @@ long long beam4_resident_waves() {
 
 static int beam4_mode() { return env_int("LLM_BEAM4", 0); }  // read per launch
 
+// LLM_BEAM4 = 2: pa_beam_mq_kernel<2, 2>; 3: <3, 1> (one page in flight, 3 waves per SIMD)
+template <int MINW, int STAGES>
 long long beam_mq_resident_waves() {
   static long long cached = 0;
   if (cached) return cached;
   int dev = 0, cus = 0, blocks = 0;
   if (hipGetDevice(&dev) == hipSuccess &&
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, pa_beam_mq_kernel<BEAM_MQ_MINW>, 256, 0) ==
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, pa_beam_mq_kernel<MINW, STAGES>, 256, 0) ==
           hipSuccess &&
       cus > 0 && blocks > 0) {
     cached = (long long)cus * blocks * 4;
@@ -980,7 +991,8 @@ long long beam_mq_resident_waves() {
 }
 
 long long tune_beam4_resident_for(int D, int TS) {
-  if (beam4_mode() == 2 && D == 128 && TS == 16) return beam_mq_resident_waves();
+  if (beam4_mode() == 2 && D == 128 && TS == 16) return beam_mq_resident_waves<2, 2>();
+  if (beam4_mode() == 3 && D == 128 && TS == 16) return beam_mq_resident_waves<3, 1>();
   auto by_ts = [&](auto d) -> long long {
     constexpr int DD = decltype(d)::value;
     return TS == 16 ? beam4_resident_waves<DD, 16>() : beam4_resident_waves<DD, 32>();
@@ -997,7 +1009,11 @@ hipError_t tune_launch_beam4(const PaSplitArgs& a, int D, int TS, hipStream_t st
   const int waves4 = ((a.B + 3) / 4) * a.H * a.nsplit;
   const dim3 grid((waves4 + 3) / 4), block(256);
   if (beam4_mode() == 2 && D == 128 && TS == 16) {
-    hipLaunchKernelGGL((pa_beam_mq_kernel<BEAM_MQ_MINW>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((pa_beam_mq_kernel<2, 2>), grid, block, 0, st, a);
+    return hipGetLastError();
+  }
+  if (beam4_mode() == 3 && D == 128 && TS == 16) {
+    hipLaunchKernelGGL((pa_beam_mq_kernel<3, 1>), grid, block, 0, st, a);
     return hipGetLastError();
   }
   auto go = [&](auto d, auto ts) {
@@ -1036,6 +1052,31 @@ hipError_t tune_launch_beam_loads_only(const PaSplitArgs& a, dim3 grid, hipStrea
 #endif
   hipLaunchKernelGGL((pa_split_kernel<128, 16, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
                                       true, true>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// The shipped BEAM form with its shared chunks delivered by an LDS-DMA ring
+// of `ring` 8 KiB chunks (pa_split_kernel RING; LLM_BEAM_RING = 3 / 4 / 6 / 8,
+// LLM_BEAM_DIAG = 2: the same with a trivial consumer).
+hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st, int ring,
+                                 bool load_only) {
+  auto go = [&](auto r, auto lo) {
+    constexpr int R = decltype(r)::value;
+    constexpr bool LO = decltype(lo)::value;
+    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, LO, true, LLM_F16,
+                                        true, false, false, 0, R>),
+                       grid, dim3(256), 0, st, a);
+  };
+  auto by_ring = [&](auto lo) {
+    switch (ring) {
+      case 3: go(std::integral_constant<int, 3>{}, lo); break;
+      case 6: go(std::integral_constant<int, 6>{}, lo); break;
+      case 8: go(std::integral_constant<int, 8>{}, lo); break;
+      default: go(std::integral_constant<int, 4>{}, lo); break;
+    }
+  };
+  if (load_only) by_ring(std::true_type{});
+  else by_ring(std::false_type{});
   return hipGetLastError();
 }
 

@@ -16,5 +16,9 @@ hipError_t tune_beam_mfma_occupancy(int* blocks);
 // the shipped BEAM form of pa_split_kernel (D 128, page 16) with a trivial
 // consumer (LOAD_ONLY): its loads, LDS staging and barriers without the maths
 hipError_t tune_launch_beam_loads_only(const PaSplitArgs& a, dim3 grid, hipStream_t st);
+// the same form with the shared chunks delivered by an LDS-DMA ring of `ring`
+// chunks (pa_split_kernel RING), optionally with the trivial consumer
+hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st, int ring,
+                                 bool load_only);
 
 }  // namespace llm

@@ -96,8 +96,8 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     shared page, and never-written (NaN) token rows past every context in both
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
     cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1),
-    its one-wave-per-group kernel (LLM_BEAM4=1) and that schedule with MFMA
-    q.k (LLM_BEAM4=2)."""
+    its one-wave-per-group kernel (LLM_BEAM4=1) and the shipped form fed by an
+    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits)."""
     import torch
     import llm_capi
     rng = np.random.default_rng(B * 7 + T)
@@ -171,12 +171,13 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     assert np.isfinite(out4).all()
     assert_parity(out4, ref, 1e-3)
     assert rel_err(out4, plain) < 1e-5
-    # ... and the same schedule with the 4 beams' q.k on the matrix cores
-    # (pa_beam_mq_kernel, LLM_BEAM4=2; D 128, page 16)
-    monkeypatch.setenv("LLM_BEAM4", "2")
-    outq = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
-                              beam_ids=d(beam_ids), row_group=4,
-                              lib=llm_capi.load_tune()).cpu().numpy()
-    assert np.isfinite(outq).all()
-    assert_parity(outq, ref, 1e-3)
-    assert rel_err(outq, plain) < 1e-5
+    # ... and the shipped form with its shared chunks delivered by an LDS-DMA
+    # ring (LLM_BEAM_RING): the same arithmetic over the same bytes, so the
+    # same bits as the product launch
+    monkeypatch.setenv("LLM_BEAM4", "0")
+    for ring in (3, 4, 8):
+        monkeypatch.setenv("LLM_BEAM_RING", str(ring))
+        outr = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                                  beam_ids=d(beam_ids), row_group=4,
+                                  lib=llm_capi.load_tune()).cpu().numpy()
+        assert np.array_equal(outr.view(np.uint32), outg.view(np.uint32)), (ring, rel_err(outr, outg))

@@ -37,7 +37,7 @@ LOGIT_TOL = 1e-3
 TIE_TOL = 1e-5
 FORM_DIRECT, FORM_SPLIT_MERGE, FORM_SPLIT_MERGE_ROW, FORM_WG_MERGE, FORM_BEAM = 0, 1, 2, 3, 16
 FORM_OPROJ = 32  # FP16 decoder: o_proj fused into the workgroup merge
-FORM_QKV = 64    # ... and LN1 + the q/k/v projection + KV append in the same workgroups
+FORM_QKV = 64    # ... and LN1 + q/k/v + KV append in the same workgroups (tuning build)
 
 
 def _torch():
@@ -225,10 +225,10 @@ def test_int8_c4_beam_state_attention_vs_oracle(gpu, oracle):
 def test_f16_step_workgroup_merge_vs_oracle(gpu, oracle):
     """C2 dims (12 heads x 64, 16 rows, T 2048): the FP16 decoder's attention
     merges its splits inside the split workgroup (3 splits) and writes the
-    packed fp16 o_proj input, compared with the oracle's fp32 attention.  The
-    same workgroups normalise their rows and project q, k, v themselves
-    (LLM_PA_FORM_QKV): the tapped LN1 rows and the appended K / V are held to
-    the oracle's own within one fp16 ulp, like the GEMM inputs."""
+    packed fp16 o_proj input, compared with the oracle's fp32 attention, and
+    adds its o_proj into the fused columns (LLM_PA_FORM_OPROJ).  The tapped
+    LN1 rows and the appended K / V are held to the oracle's own within one
+    fp16 ulp, like the GEMM inputs."""
     torch = _torch()
     import llm_decoder
     from oracle.oracle import OracleDecoder
@@ -254,7 +254,7 @@ def test_f16_step_workgroup_merge_vs_oracle(gpu, oracle):
     taps = _Taps(dec, w["cfg"], rows, f16=True)
     dec.begin_synthetic(rows, T, 5, True)
     ns, form = dec.attention_plan()
-    assert form == FORM_WG_MERGE | FORM_OPROJ | FORM_QKV and 2 <= ns <= 8, (ns, form)
+    assert form == FORM_WG_MERGE | FORM_OPROJ and 2 <= ns <= 8, (ns, form)
     odec = OracleDecoder(oracle, w, rows)
     decoder_kv_to_oracle(dec, odec, rows, T)
     logits = torch.empty((rows, V), device="cuda")

