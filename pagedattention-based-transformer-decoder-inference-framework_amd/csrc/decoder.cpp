@@ -92,12 +92,6 @@ struct llm_decoder {
   DevBuf<int32_t> lm_pi;
   int lm_nwg = 0;
   DevBuf<int8_t> qa;
-  // INT8 decode rows: the LayerNorm outputs the o_proj / fc2 last-arriver
-  // seam writes (GemmArgs::lnx_*), packed int8 [B16][hid] + row scales, and
-  // its arrival counters (one per 16-row block, zero between launches)
-  DevBuf<int8_t> qa_ln;
-  DevBuf<float> sa_ln;
-  DevBuf<unsigned> lnx_cnt;
   DevBuf<uint16_t> a16;
   // FP16: the fused o_proj's int64 columns [max_batch][hid] (zero between
   // attention launches: the adder completing a column clears it); oacc_run:
@@ -214,12 +208,6 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   RET_IF(d->sa.alloc((size_t)B));
   const size_t B16 = ((size_t)B + 15) / 16 * 16;  // packed-A tiles are 16 rows
   RET_IF(d->qa.alloc(B16 * std::max(hid, inter)));
-  if (d->wdtype == LLM_I8 && lnx_on()) {  // the LayerNorm seam (tuning build)
-    RET_IF(d->qa_ln.alloc(B16 * hid));
-    RET_IF(d->sa_ln.alloc((size_t)B));
-    RET_IF(d->lnx_cnt.alloc(B16 / 16));
-    LLM_HIP_RET(hipMemset(d->lnx_cnt.p, 0, sizeof(unsigned) * d->lnx_cnt.n));
-  }
   if (d->wdtype == LLM_F16) {
     RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
     RET_IF(d->oacc.alloc((size_t)B * hid));
@@ -419,12 +407,6 @@ struct Rows {
   void* act = nullptr;  // packed-A GEMM input (int8 or fp16), 16-row tiles
   void* act2 = nullptr; // fp16 decoder: fc2's packed input (written by fc1 while act is read)
   float* sa = nullptr;  // [n] int8 row scales
-  // INT8 decode rows, LayerNorm seam (ln_seam): LN2 (after o_proj) and the
-  // next layer's LN1 (after fc2) are computed by those GEMMs' last-arriving
-  // workgroups into act_ln / sa_ln, which fc1 and the next qkv read
-  bool ln_seam = false;
-  void* act_ln = nullptr;
-  float* sa_ln = nullptr;
   const int32_t* pos = nullptr;  // [n] position written this pass
   const int32_t* ctx = nullptr;  // [n] context length attended (pos + 1)
   const int32_t* beam_rows = nullptr;  // page-table row per row; NULL: table_row0 + m
@@ -484,12 +466,7 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   g.C = R.q; g.c_cols = hid; g.c_ld = hid;  // q only: K and V go straight into the pages
   g.kv = &app;
   if (wdtype == LLM_I8) g.sa = R.sa, g.sw = sw_qkv.p + (size_t)l * 3 * hid;
-  if (R.ln_seam && l > 0) {  // LN1 was written by the previous layer's fc2 (seam)
-    g.A = R.act_ln;
-    g.sa = R.sa_ln;
-  } else {
-    RET_IF(layer_norm_into(g, R, ln1_g.p + lh, ln1_b.p + lh, st));
-  }
+  RET_IF(layer_norm_into(g, R, ln1_g.p + lh, ln1_b.p + lh, st));
   RET_IF(weight_gemm(g, st));
   return tap(l, 0, R, hid, st);
 }
@@ -638,21 +615,11 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
     g.ln_quant_only = 1;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
   }
-  if (R.ln_seam) {  // LN2 by o_proj's last-arriving workgroups
-    g.lnx_g = ln2_g.p + lh; g.lnx_b = ln2_b.p + lh;
-    g.lnx_act = R.act_ln; g.lnx_sa = R.sa_ln; g.lnx_cnt = lnx_cnt.p;
-  }
   if (!R.oacc) RET_IF(weight_gemm(g, st));  // (fused: the attention wrote x)
   g.ln_x = nullptr; g.ln_quant_only = 0; g.act_out = nullptr; g.sa_out = nullptr;
-  g.lnx_cnt = nullptr;
   RET_IF(tap(l, 1, R, hid, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
-  if (R.ln_seam) {
-    g.A = R.act_ln;
-    g.sa = R.sa_ln;
-  } else {
-    RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
-  }
+  RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
   if (i8) {
@@ -677,11 +644,6 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
-  if (R.ln_seam && l + 1 < L) {  // the next layer's LN1 by fc2's last-arriving workgroups
-    const size_t ln = (size_t)(l + 1) * hid;
-    g.lnx_g = ln1_g.p + ln; g.lnx_b = ln1_b.p + ln;
-    g.lnx_act = R.act_ln; g.lnx_sa = R.sa_ln; g.lnx_cnt = lnx_cnt.p;
-  }
   return weight_gemm(g, st);
 }
 
@@ -696,12 +658,6 @@ Rows llm_decoder::step_rows(int r0, int n, uint8_t* ws) {
   R.act = wdtype == LLM_I8 ? (void*)(qa.p + (size_t)r0 * qa_ld) : (void*)(a16.p + (size_t)r0 * qa_ld);
   if (wdtype == LLM_F16) R.act2 = a16.p + (b16 + (size_t)r0) * qa_ld;
   R.sa = sa.p + r0;
-  if (wdtype == LLM_I8 && lnx_on() && !ln_fusable(wdtype, n, hid) && lnx_ok(wdtype, n, hid, hid) &&
-      lnx_ok(wdtype, n, hid, inter) && lnx_cnt.p) {  // (o_proj and fc2)
-    R.ln_seam = true;
-    R.act_ln = qa_ln.p + (size_t)r0 * hid;
-    R.sa_ln = sa_ln.p + r0;
-  }
   R.pos = pos.p + r0;
   R.ctx = ctx.p + r0;
   R.table_row0 = r0;
@@ -723,12 +679,11 @@ int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
   const size_t slot = (size_t)l * 4 + stage;
   const size_t n16 = ((size_t)R.n + 15) / 16 * 16;
   const size_t r0 = (size_t)R.table_row0;  // rows r0.. of the step (16-row aligned)
-  const bool seam = R.ln_seam && (stage == 2 || (stage == 0 && l > 0));  // LN written by a seam
-  const void* src = seam ? R.act_ln : f16 && (stage == 3 || (stage == 0 && R.qkv_fused)) ? R.act2 : R.act;
+  const void* src = f16 && (stage == 3 || (stage == 0 && R.qkv_fused)) ? R.act2 : R.act;
   LLM_HIP_RET(hipMemcpyAsync(tap_q + (slot * b16 * qa_ld + r0 * K) * es, src, n16 * K * es,
                              hipMemcpyDeviceToDevice, st));
   if (!f16)
-    LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, seam ? R.sa_ln : R.sa, sizeof(float) * R.n,
+    LLM_HIP_RET(hipMemcpyAsync(tap_s + slot * maxB + r0, R.sa, sizeof(float) * R.n,
                                hipMemcpyDeviceToDevice, st));
   return LLM_OK;
 }
@@ -945,7 +900,6 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
   if (d->oacc.p) LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * d->oacc.n));
   if (d->oflag.p) LLM_HIP_RET(hipMemset(d->oflag.p, 0, sizeof(int)));
-  if (d->lnx_cnt.p) LLM_HIP_RET(hipMemset(d->lnx_cnt.p, 0, sizeof(unsigned) * d->lnx_cnt.n));
   std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
   LLM_HIP_RET(hipMemcpy(d->pos.p, pos.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
   LLM_HIP_RET(hipMemcpy(d->ctx.p, ctx.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));

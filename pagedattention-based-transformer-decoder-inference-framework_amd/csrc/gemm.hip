@@ -108,28 +108,6 @@ bool llm::quant_prologue_ok(int M, int N, int K) {
          (size_t)rows * (ln_row_stride(K, 1) + 4) <= kLnLdsMax;
 }
 
-// The last-arriver LayerNorm seam (GemmArgs::lnx_*): the workgroup completing
-// a row block normalises its rows one wave per row with ln_wave's 8 float4
-// chunks per lane, so N <= 2048; the packed-A output needs N % 64 == 0; and
-// the launch must tile the rows 16 per workgroup (M <= 16, or the 16-row
-// forms of 17..64 rows, narrow_tile_for), so a last arriver normalises 16
-// rows, not 64.
-bool llm::lnx_ok(int dtype, int M, int N, int K) {
-  if (dtype != LLM_I8 || M <= 0 || M > 64 || N % 64 != 0 || N > 2048) return false;
-  TileChoice t{0, 0, 0};
-  return M <= 16 || (narrow_tile_for(M, N, K, t) && t.mrows == 16);
-}
-
-// Tuning build only (LLM_LNX=1): same-box it lost C4 -10 % and C3 -1 %
-// against the LayerNorm launches it replaces.
-bool llm::lnx_on() {
-#if LLM_TUNING
-  return env_int("LLM_LNX", 0) != 0;  // read per call: an A/B flips it in-process
-#else
-  return false;
-#endif
-}
-
 int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   LLM_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0 && (g.A || g.ln_x) && g.W_packed,
               "weight_gemm: bad arguments");
@@ -159,17 +137,6 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;
   a.w_keep = g.w_keep;
-  if (g.lnx_cnt) {
-    LLM_REQUIRE(lnx_ok(g.dtype, g.M, g.N, g.K) && g.C && (g.c_cols <= 0 || g.c_cols == g.N) &&
-                    (g.c_ld <= 0 || g.c_ld == g.N) && !g.kv && g.lnx_g && g.lnx_b && g.lnx_act &&
-                    g.lnx_sa,
-                "weight_gemm: the LayerNorm seam needs an I8 GEMM of 16-row tiles writing whole rows "
-                "of N <= 2048 (N % 64 == 0), gamma / beta and its outputs");
-    a.lnx_g = g.lnx_g; a.lnx_b = g.lnx_b; a.lnx_eps = g.lnx_eps;
-    a.lnx_act = static_cast<uint8_t*>(g.lnx_act);
-    a.lnx_sa = g.lnx_sa;
-    a.lnx_cnt = g.lnx_cnt;
-  }
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");

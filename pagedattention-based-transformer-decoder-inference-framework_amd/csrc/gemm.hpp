@@ -59,16 +59,6 @@ struct WeightGemm {
   // ln_b unused) -- the o_proj prologue replacing the attention merge's
   // quantisation (quant_prologue_ok)
   int ln_quant_only = 0;
-  // I8: last-arriver LayerNorm + quantisation of the output rows into the
-  // next GEMM's packed A (lnx_act) and row scales (lnx_sa), gamma / beta
-  // lnx_g / lnx_b, arrival counters lnx_cnt (zero between launches; one per
-  // row block) -- GemmArgs::lnx_*, lnx_ok
-  const float* lnx_g = nullptr;
-  const float* lnx_b = nullptr;
-  float lnx_eps = 1e-5f;
-  void* lnx_act = nullptr;
-  float* lnx_sa = nullptr;
-  unsigned* lnx_cnt = nullptr;
 };
 
 // Input of a LayerNorm when it is not x: embedding rows E[tok[r]] (the decode
@@ -80,12 +70,6 @@ struct LnSource {
 };
 
 int weight_gemm(const WeightGemm& g, hipStream_t st);
-// Whether an I8 weight GEMM of M rows, N output columns and K inputs can end
-// in the last-arriver LayerNorm seam (WeightGemm::lnx_*): N <= 2048, N % 64 ==
-// 0, and the launch tiles the rows 16 per workgroup.
-bool lnx_ok(int dtype, int M, int N, int K);
-// Whether the LNX seam is switched on (tuning build: LLM_LNX=0 switches it off).
-bool lnx_on();
 // Whether weight_gemm can run the LayerNorm prologue for M rows of K (the
 // per-workgroup A image must fit in LDS; K <= 128 groups of 16 bytes).
 bool ln_fusable(int dtype, int M, int K);

@@ -95,46 +95,7 @@ struct GemmArgs {
   unsigned* seam;
   int seam_n;
   int qdiag;  // tuning build, timing only: bit0 skip the prologue, bit1 no weight loads before it
-  // Last-arriver LayerNorm of the output rows (gemm_kernel<..., LNX = 1>, I8,
-  // no split-K): C rows are stored write-through (sc1); every workgroup then
-  // adds one arrival to lnx_cnt[row block] (agent scope), and the workgroup
-  // completing a row block normalises its 16 MT rows (lnx_g / lnx_b, as the
-  // LayerNorm launch) and quantises them into the NEXT GEMM's packed-A input
-  // lnx_act + row scales lnx_sa, then resets the counter.  Nobody waits: the
-  // other workgroups exit.  Replaces the LayerNorm launch after o_proj (LN2)
-  // and after fc2 (the next layer's LN1).
-  const float* lnx_g;
-  const float* lnx_b;
-  float lnx_eps;
-  uint8_t* lnx_act;
-  float* lnx_sa;
-  unsigned* lnx_cnt;
 };
-
-// The LNX seam's C store: write-through (sc1, agent-scope relaxed atomic
-// store of the global address: MI355X_MICROARCH.md visibility rows), so the
-// last arriver on another CU / XCD reads it with sc1 loads and no fence.
-__device__ __forceinline__ void store_sc1(float* p, float v) {
-  typedef __attribute__((address_space(1))) float gfloat;
-  __hip_atomic_store((gfloat*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One row of fp32 C as ln_wave chunks, every load sc1 (bypassing this CU's
-// L1 and this XCD's L2: the row was written by other workgroups in this
-// launch).
-template <int CPL>
-__device__ __forceinline__ void ln_wave_load_sc1(const float* row, int K4, LnRow<CPL>& r) {
-  const int lane = lane_id();
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, (uint32_t)K4 * 16u,
-                                                    0x00020000);
-#pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = 64 * j + lane;
-    r.v[j] = c < K4 ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rs, (uint32_t)c * 16u, 0, 16))
-                    : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
 
 // LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
 // stride K * ESIZE + 32 bytes.  With that stride (K * ESIZE a multiple of 256)
@@ -285,8 +246,7 @@ __device__ __forceinline__ void seam_wait(unsigned* ctr, int n) {
   __syncthreads();
 }
 
-template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0, int SEAM = 0,
-          int LNX = 0>
+template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0, int SEAM = 0>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int bz, int nz,
                                           int gx) {
   using Tr = GemmTraits<KIND>;
@@ -584,11 +544,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int
       y = a.bias ? s + e_bias[e] : s;
     }
     y = apply_act(y, a.act);
-    if constexpr (LNX != 0) {
-      store_sc1(a.C + (size_t)m * a.c_ld + n, y);
-    } else {
-      if (a.C && n < a.c_cols) a.C[(size_t)m * a.c_ld + n] = y;
-    }
+    if (a.C && n < a.c_cols) a.C[(size_t)m * a.c_ld + n] = y;
     if (a.c16) a.c16[a_frag_off_f16(m, n, a.N >> 5)] = (_Float16)y;
     if (e_page[e] >= 0) {
       const int which = n >= 2 * hid;  // 0: K, 1: V
@@ -600,47 +556,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int
     }
   }
   if (stamp && lane == 0) stamp[32 + w] = phase_clock();  // [32, 48): wave end
-  if constexpr (LNX != 0) {
-    // every storing wave drains its sc1 stores, then ONE arrival per workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __shared__ int lnx_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned old =
-          __hip_atomic_fetch_add(a.lnx_cnt + by, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lnx_last = old == (unsigned)gx - 1u;
-    }
-    __syncthreads();
-    if (!lnx_last) return;
-    if (threadIdx.x == 0) __hip_atomic_store(a.lnx_cnt + by, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the row block's 16 MT rows: wave w takes rows w, w + WAVES, ... (every
-    // load of C sc1; LayerNorm + quantisation as layernorm_rows_kernel /
-    // ln_prologue: ln_wave.hpp, bit-identical)
-    constexpr int CPL = 8;  // N <= 2048 (lnx_ok)
-    const int K4 = a.N >> 2, KSn = a.N >> 6;
-    LnRow<CPL> gm, bt;
-    ln_wave_load(a.lnx_g, K4, true, gm);
-    ln_wave_load(a.lnx_b, K4, true, bt);
-    for (int r = w; r < 16 * MT; r += WAVES) {
-      const int m = m0 + r;
-      if (m >= a.M) break;
-      LnRow<CPL> x;
-      ln_wave_load_sc1(a.C + (size_t)m * a.c_ld, K4, x);
-      const float am = ln_wave_compute(x, gm, bt, a.N, a.lnx_eps);
-      const float scale = 127.f / (am + 1e-6f);
-#pragma unroll
-      for (int j = 0; j < CPL; ++j) {
-        const int c = 64 * j + lane;
-        if (c < K4)
-          *reinterpret_cast<uint32_t*>(a.lnx_act + a_frag_off_i8(m, 4 * c, KSn)) =
-              ln_quant4(x.v[j], scale);
-      }
-      if (lane == 0) a.lnx_sa[m] = 1.0f / scale;
-    }
-  }
 }
 
-template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0, int LNX = 0>
+template <GemmKind KIND, int MT, int NT, int WAVES, int DIAG = 0, int PRO = 0>
 __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
 #if LLM_TUNING
@@ -654,7 +572,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_kernel(GemmArgs a) {
     by = tile / (int)gridDim.x;
   }
 #endif
-  gemm_tile<KIND, MT, NT, WAVES, DIAG, PRO, 0, LNX>(a, bx, by, bz, (int)gridDim.z, (int)gridDim.x);
+  gemm_tile<KIND, MT, NT, WAVES, DIAG, PRO>(a, bx, by, bz, (int)gridDim.z, (int)gridDim.x);
 }
 
 // Repack W [K][N] (row-major) into per-(16-col tile, k-step) 1 KiB blocks,
@@ -707,32 +625,10 @@ hipError_t launch_gemm_nt(const GemmArgs& a, int waves, int mblocks, hipStream_t
   if constexpr (NT <= 2) {
     if (a.ln_x) {
       const size_t lds = ln_lds_bytes<KIND, MT, NT, 8>(a.K);
-#if LLM_TUNING
-      if constexpr (KIND == GemmKind::I8) {
-        if (a.lnx_cnt) {  // + the last-arriver LayerNorm seam (tuning build)
-          hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1, 1>), grid, dim3(512), lds, st, a);
-          return hipGetLastError();
-        }
-      }
-#endif
       hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 1>), grid, dim3(512), lds, st, a);
       return hipGetLastError();
     }
   }
-#if LLM_TUNING
-  if constexpr (KIND == GemmKind::I8 && NT <= 2) {
-    if (a.lnx_cnt) {  // the last-arriver LayerNorm seam (tuning build; no split-K: lnx_ok)
-      if constexpr (MT * NT * 8 <= 64) {
-        if (waves != 4) {
-          hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 8, 0, 0, 1>), grid, dim3(512), 0, st, a);
-          return hipGetLastError();
-        }
-      }
-      hipLaunchKernelGGL((gemm_kernel<KIND, MT, NT, 4, 0, 0, 1>), grid, dim3(256), 0, st, a);
-      return hipGetLastError();
-    }
-  }
-#endif
   // the cross-wave sums' static LDS (WAVES x MT NT KiB) must stay <= 64 KiB
   if constexpr (MT * NT * 8 <= 64) {
     if (waves != 4) {

@@ -400,6 +400,10 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
         *beam = true;
         return tune_launch_beam_loads_only(a, grid, st);
       }
+      if (env_int("LLM_BEAM_STAMPS", 0) == 1) {  // per-wave timestamps (scripts/beam_stamps.py)
+        *beam = true;
+        return tune_launch_beam_stamps(a, grid, st);
+      }
       const int ring = env_int("LLM_BEAM_RING", 0);
       if (ring > 0) {  // shared chunks through an LDS-DMA ring
         *beam = true;
@@ -736,6 +740,11 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     if (nw >= nsplit && (long long)nw * kMaxPps >= ntiles_max) nsplit = nw;
   }
 #if LLM_TUNING
+  // tuning build: LLM_BEAM_NSPLIT forces the split count of beam-group launches
+  if (row_group == 4 && pps_fixed <= 0) {
+    const int f = env_int("LLM_BEAM_NSPLIT", 0);
+    if (f >= 2 && (long long)f * kMaxPps >= ntiles_max) nsplit = std::min(f, kMaxSplits);
+  }
   // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
   // eligible launches (fp16 row outputs, dynamic splits)
   if (rows && (rows->out16 || oproj) && !rows->q && row_group == 1 && pps_fixed <= 0) {

@@ -102,6 +102,10 @@ struct PaSplitArgs {
   float ln_eps;
   const _Float16* qkv_w;    // [H][hid/8][3D][8]: column c = q (c < D), k (< 2D), v
   _Float16* ln_tap;         // optional: LN1 rows in packed-A order (taps), head 0 writes
+  // tuning (pa_split_kernel STAMPS): per wave wid, s_memrealtime (100 MHz) at
+  // entry, at the first KV load, after the shared-prefix chunks, at exit, and
+  // the wave's HW_ID (CU / SIMD / XCC placement): stamps[wid * 5 + 0..4]
+  unsigned long long* stamps;
 };
 
 constexpr int kQkvMaxHid = 2048;  // fused q/k/v: the LN1 row in LDS as fp16
@@ -281,7 +285,7 @@ __device__ __forceinline__ void qkv_prologue(const PaSplitArgs& a, int b, int h,
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int QKV = 0, int RING = 0>
+          int QKV = 0, int RING = 0, bool STAMPS = false>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -298,6 +302,7 @@ void pa_split_kernel(PaSplitArgs a) {
   static_assert(!(WGM && (DIRECT || BEAM)), "the workgroup merge is a split form");
   static_assert(!OPROJ || (WGM && KVT == LLM_F16), "the fused o_proj is a workgroup-merge form");
   static_assert(QKV == 0 || OPROJ, "the fused q/k/v projection is an o_proj-fused form");
+  const unsigned long long t_entry = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int lane = lane_id();
   const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
   const int G = BEAM ? 4 : WGM ? 1 : a.group;
@@ -573,6 +578,11 @@ void pa_split_kernel(PaSplitArgs a) {
 
   const int nchunks = (count + U - 1) / U;
   int ch0 = 0;  // first chunk of the per-wave direct path
+  unsigned long long t_load = 0, t_shared = 0;
+  if constexpr (STAMPS) {
+    (void)page_of(0);  // the page ids have arrived
+    t_load = __builtin_amdgcn_s_memrealtime();
+  }
   if constexpr (BEAM) {
     static_assert(NR % 2 == 0, "beam prefetch splits a chunk's 2*NR pieces in quarters");
     constexpr int QP = NR / 2;  // pieces per wave per chunk
@@ -705,6 +715,7 @@ void pa_split_kernel(PaSplitArgs a) {
       ch0 = nsh;
     }
   }
+  if constexpr (STAMPS) t_shared = __builtin_amdgcn_s_memrealtime();
   if constexpr (STAGES == 1) {
     u32x4 kA[NR], vA[NR];
     for (int ch = ch0; ch < nchunks; ++ch) {
@@ -919,6 +930,19 @@ void pa_split_kernel(PaSplitArgs a) {
         a.part_ml[pidx * 2] = m;
         a.part_ml[pidx * 2 + 1] = l;
       }
+    }
+  }
+  if constexpr (STAMPS) {
+    if (lane == 0) {
+      unsigned long long* st = a.stamps + (size_t)wid * 5;
+      st[0] = t_entry;
+      st[1] = t_load;
+      st[2] = t_shared;
+      st[3] = __builtin_amdgcn_s_memrealtime();
+      unsigned hw = 0, xcc = 0;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      st[4] = ((unsigned long long)xcc << 32) | hw;
     }
   }
 }

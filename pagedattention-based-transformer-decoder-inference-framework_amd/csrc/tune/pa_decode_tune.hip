@@ -1080,6 +1080,33 @@ hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st
   return hipGetLastError();
 }
 
+// The shipped BEAM form with per-wave timestamps (pa_split_kernel STAMPS,
+// LLM_BEAM_STAMPS=1): entry / first KV load / shared prefix done / exit, and
+// the wave's HW_ID, into a buffer pa_tune_stamps() copies out (diagnostics:
+// allocates on first use, so not inside a graph capture).
+static unsigned long long* g_stamps = nullptr;
+static size_t g_stamps_cap = 0, g_stamps_waves = 0;
+
+hipError_t tune_launch_beam_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t st) {
+  const size_t waves = (size_t)grid.x * 4;
+  if (waves > g_stamps_cap) {
+    if (g_stamps) (void)hipFree(g_stamps);
+    g_stamps = nullptr;
+    g_stamps_cap = 0;
+    if (hipMalloc(&g_stamps, waves * 5 * sizeof(unsigned long long)) != hipSuccess)
+      return hipErrorOutOfMemory;
+    g_stamps_cap = waves;
+  }
+  (void)hipMemsetAsync(g_stamps, 0, waves * 5 * sizeof(unsigned long long), st);
+  PaSplitArgs a = a0;
+  a.stamps = g_stamps;
+  g_stamps_waves = waves;
+  hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
+                                      true, false, false, 0, 0, true>),
+                     grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t tune_beam_mfma_occupancy(int* blocks) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, pa_beam_mfma_kernel<0>, 256, 0);
 }
@@ -1087,6 +1114,19 @@ hipError_t tune_beam_mfma_occupancy(int* blocks) {
 }  // namespace llm
 
 using namespace llm;
+
+// Tuning hook: the last LLM_BEAM_STAMPS launch's per-wave stamps (5 per wave,
+// pa_split_kernel STAMPS) into host (room for max_waves); returns the waves
+// copied (-1: none recorded).
+extern "C" long long pa_tune_stamps(unsigned long long* host, long long max_waves) {
+  if (!g_stamps || !host) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const size_t n = std::min<size_t>((size_t)max_waves, g_stamps_waves);
+  if (hipMemcpy(host, g_stamps, n * 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return -1;
+  return (long long)n;
+}
 
 // Tuning hook (not part of include/llm_decoder.h): run the split kernel of
 // D=128 / TS=16 in a given variant so scripts/bench_kernels.py can compare

@@ -18,6 +18,8 @@ hipError_t tune_beam_mfma_occupancy(int* blocks);
 hipError_t tune_launch_beam_loads_only(const PaSplitArgs& a, dim3 grid, hipStream_t st);
 // the same form with the shared chunks delivered by an LDS-DMA ring of `ring`
 // chunks (pa_split_kernel RING), optionally with the trivial consumer
+// the shipped form with per-wave timestamps (STAMPS; pa_tune_stamps copies them)
+hipError_t tune_launch_beam_stamps(const PaSplitArgs& a, dim3 grid, hipStream_t st);
 hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st, int ring,
                                  bool load_only);
 
