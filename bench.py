@@ -194,16 +194,14 @@ FORM_OUT = {"INT8Decoder": {0: " (fp32 rows; the o_proj prologue quantises them)
             "CUDADecoder": {3: " (packed fp16 o_proj input)"}}
 # form bit 32: the FP16 decoder's o_proj runs inside the workgroup merge
 OPROJ_OUT = " (o_proj fused: each (row, head) workgroup adds o_h W_o[h] into int64 rows)"
-# form bit 64: ... and normalises its row and projects its head's q, k, v itself
-QKV_OUT = " (LN1 + q/k/v projection + KV append fused: each (row, head) workgroup projects its head)"
 
 
 def fused_weight_bytes(cfg, form):
-    """Unique weight bytes the fused forms of the FP16 attention launch read
-    besides the KV pages: W_o (o_proj fused, bit 32) and W_qkv (LN1 + q/k/v
-    fused, bit 64), fp16, once per launch from HBM / the Infinity Cache."""
+    """Unique weight bytes the fused form of the FP16 attention launch reads
+    besides the KV pages: W_o (o_proj fused, form bit 32), fp16, once per
+    launch from HBM / the Infinity Cache."""
     hid = cfg["H"] * cfg["D"]
-    return (2 * hid * hid if form & 32 else 0) + (2 * 3 * hid * hid if form & 64 else 0)
+    return 2 * hid * hid if form & 32 else 0
 
 
 def cpu_threads():
@@ -430,7 +428,6 @@ def main():
             "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}>"
                       + (" beam-group" if form & 16 else "") + ": " + FORM_NAMES[form & 15]
                       + (OPROJ_OUT if form & 32 else FORM_OUT.get(cfg["cls"], {}).get(form & 15, ""))
-                      + (QKV_OUT if form & 64 else "")
                       + f", {nsplit} splits (the step's own launch, llm_decoder_run_attention)",
             "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
     if "beams" in cfg:  # logical bytes: every beam reads its whole context

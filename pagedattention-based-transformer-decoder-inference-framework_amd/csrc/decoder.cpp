@@ -76,9 +76,6 @@ struct llm_decoder {
   // FP16: W_o again as per-head column slices for the fused o_proj,
   // [L][H][D/8][hid][8] (PaRowOutputs::wo_heads)
   DevBuf<uint16_t> wo_heads;
-  // FP16: W_qkv again as per-head column slices for the fused LN1 + q/k/v
-  // projection, [L][H][hid/8][3D][8] (PaRowOutputs::qkv_w)
-  DevBuf<uint16_t> wqkv_heads;
   size_t sz_qkv = 0, sz_o = 0, sz_1 = 0, sz_2 = 0;
   bool weights_ready = false;
   int w_keep = 0;  // the GEMM weights fit the Infinity Cache: keep them there (w_keep_for)
@@ -120,7 +117,6 @@ struct llm_decoder {
   int layer_norm_into(WeightGemm& g, const struct Rows& R, const float* gamma, const float* beta,
                       hipStream_t st);
   LnSource embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
-  LnSource attn_src;   // fused q/k/v: layer 0's attention reads E[token] rows itself
 
   ~llm_decoder() {
     if (h_oflag) (void)hipHostFree(h_oflag);
@@ -144,7 +140,6 @@ struct llm_decoder {
   int layer_attn(int l, hipStream_t st, const struct Rows& R, PaPlan* plan = nullptr);
   bool quant_prologue(const struct Rows& R) const;
   bool oproj_fusable(const struct Rows& R);
-  void fuse_decode_rows(struct Rows& R, float* oproj_out, long long* acc);
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -360,28 +355,6 @@ extern "C" int llm_decoder_set_f16_weights(llm_decoder* d, const llm_f16_weights
                             sizeof(uint16_t) * hid * hid, hipMemcpyHostToDevice));
     }
   }
-  // the fused q/k/v projection's head slices: [h][kg][c][j] = W_qkv[8 kg + j][col(h, c)],
-  // c < D the head's q columns, then its k and its v columns (a second copy of
-  // W_qkv, L * 3 hid^2 fp16, only where the fused form can run)
-  d->wqkv_heads.alloc(0);
-  if (d->wo_heads.p && hid <= 2048 && qkv_fuse_on()) {
-    const int D = d->D, KG = hid / 8, NC = 3 * D;
-    const uint16_t* src = static_cast<const uint16_t*>(w->wqkv);
-    std::vector<uint16_t> sl((size_t)hid * 3 * hid);
-    RET_IF(d->wqkv_heads.alloc((size_t)L * hid * 3 * hid));
-    for (int l = 0; l < L; ++l) {
-      const uint16_t* wl = src + (size_t)l * hid * 3 * hid;
-      for (int h = 0; h < d->H; ++h)
-        for (int kg = 0; kg < KG; ++kg)
-          for (int c = 0; c < NC; ++c) {
-            const size_t n = (size_t)(c / D) * hid + (size_t)h * D + c % D;
-            for (int j = 0; j < 8; ++j)
-              sl[(((size_t)h * KG + kg) * NC + c) * 8 + j] = wl[(size_t)(8 * kg + j) * 3 * hid + n];
-          }
-      LLM_HIP_RET(hipMemcpy(d->wqkv_heads.p + (size_t)l * hid * 3 * hid, sl.data(),
-                            sizeof(uint16_t) * hid * 3 * hid, hipMemcpyHostToDevice));
-    }
-  }
   RET_IF(upload_packed(d->w1, d->sz_1, w->w1, L, hid, inter, LLM_F16, "w1"));
   RET_IF(upload_packed(d->w2, d->sz_2, w->w2, L, inter, hid, LLM_F16, "w2"));
   RET_IF(upload(d->b1, w->b1, (size_t)L * inter, "b1"));
@@ -423,9 +396,6 @@ struct Rows {
   // scratch row for llm_decoder_run_attention); no o_proj launch
   long long* oacc = nullptr;
   float* oproj_out = nullptr;
-  // ... and, with it, LN1 + the q/k/v projection + the KV append (qkv_fused):
-  // no q/k/v GEMM launch; the step's first attention reads E[token] rows
-  bool qkv_fused = false;
 };
 
 // Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
@@ -436,11 +406,6 @@ struct Rows {
 // elements).
 int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
   const size_t lh = (size_t)l * hid;
-  if (R.qkv_fused) {  // the attention's workgroups normalise and project their rows themselves
-    attn_src = embed_src;
-    embed_src = LnSource{};
-    return LLM_OK;
-  }
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
   KvAppendView app;
@@ -518,20 +483,9 @@ bool llm_decoder::oproj_fusable(const Rows& R) {
   Rows r = R;
   r.oacc = oacc.p;
   r.oproj_out = R.x;
-  r.qkv_fused = false;
   PaPlan p;
   if (layer_attn(0, stream, r, &p) != LLM_OK) return false;
   return (p.form & LLM_PA_FORM_OPROJ) != 0;
-}
-
-// Decode rows whose o_proj runs in the attention's workgroup merge (into the
-// columns acc, writing oproj_out) and, where the per-head W_qkv slices exist,
-// whose LN1 + q/k/v projection + KV append run in the same workgroups.
-void llm_decoder::fuse_decode_rows(Rows& R, float* oproj_out, long long* acc) {
-  if (!oproj_fusable(R)) return;
-  R.oacc = acc;
-  R.oproj_out = oproj_out;
-  R.qkv_fused = wqkv_heads.p != nullptr;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
@@ -570,30 +524,13 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
     ro.wo_heads = wo_heads.p + (size_t)l * hid * hid;
     ro.o_n = hid;
     ro.o_flag = oflag.p;
-    if (R.qkv_fused) {
-      ro.qkv_w = wqkv_heads.p + (size_t)l * hid * 3 * hid;
-      ro.ln_x = R.x;
-      if (attn_src.emb) {
-        ro.ln_emb = attn_src.emb;
-        ro.ln_tok = attn_src.tok;
-        ro.ln_V = attn_src.V;
-      }
-      if (!plan) attn_src = LnSource{};
-      ro.ln_g = ln1_g.p + (size_t)l * hid;
-      ro.ln_b = ln1_b.p + (size_t)l * hid;
-      ro.ln_eps = 1e-5f;
-      ro.ln_tap = tap_q ? R.act2 : nullptr;  // (R.act takes the attention rows)
-    }
     ro.out16 = tap_q ? R.act : nullptr;  // the taps read the packed o_proj input
   } else {
     ro.out16 = R.act;
   }
-  RET_IF(pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
+  return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
-                            R.row_group, plan));
-  // the fused form wrote the LN1 rows (the q/k/v GEMM's A) for the taps
-  if (R.qkv_fused && !plan) RET_IF(tap(l, 0, R, hid, st));
-  return LLM_OK;
+                            R.row_group, plan);
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
@@ -635,8 +572,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   RET_IF(tap(l, 2, R, hid, st));
   g.ln_x = nullptr; g.ln_emb = nullptr; g.act_out = nullptr; g.sa_out = nullptr;
   g.C16 = nullptr;
-  g.A = i8 ? R.act : R.act2;
-  g.sa = R.sa;
+  if (!i8) g.A = R.act2;
   // quantise h1 -> mlp_fc2 (+b2)
   if (i8)
     LLM_HIP_RET(launch_quantize_rows(R.h1, R.n, inter, static_cast<int8_t*>(R.act), R.sa, st, 1));
@@ -679,7 +615,7 @@ int llm_decoder::tap(int l, int stage, const Rows& R, int K, hipStream_t st) {
   const size_t slot = (size_t)l * 4 + stage;
   const size_t n16 = ((size_t)R.n + 15) / 16 * 16;
   const size_t r0 = (size_t)R.table_row0;  // rows r0.. of the step (16-row aligned)
-  const void* src = f16 && (stage == 3 || (stage == 0 && R.qkv_fused)) ? R.act2 : R.act;
+  const void* src = f16 && stage == 3 ? R.act2 : R.act;
   LLM_HIP_RET(hipMemcpyAsync(tap_q + (slot * b16 * qa_ld + r0 * K) * es, src, n16 * K * es,
                              hipMemcpyDeviceToDevice, st));
   if (!f16)
@@ -729,7 +665,7 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
 // One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
   Rows R = step_rows(0, batch, attn_ws.p);
-  fuse_decode_rows(R, R.x, oacc.p);
+  if (oproj_fusable(R)) R.oacc = oacc.p, R.oproj_out = R.x;
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -1010,7 +946,7 @@ extern "C" int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form
   std::lock_guard<std::mutex> g(d->mu);
   LLM_REQUIRE(d->batch > 0, "llm_decoder_attention_plan: no active rows");
   Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
-  d->fuse_decode_rows(R, R.x, d->oacc.p);
+  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.x;
   PaPlan p;
   RET_IF(d->layer_attn(0, d->stream, R, &p));
   *nsplit = p.nsplit;
@@ -1033,16 +969,7 @@ extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream
       RET_IF(d->oacc_run.alloc(d->oacc.n));
       LLM_HIP_RET(hipMemset(d->oacc_run.p, 0, sizeof(long long) * d->oacc_run.n));
     }
-    d->fuse_decode_rows(R, R.o, d->oacc_run.p);
-    // the fused q/k/v form normalises x (layer 0: the next tokens' embedding
-    // rows) and appends k, v at each row's next position, which the next step
-    // overwrites
-    if (R.qkv_fused && layer == 0) {
-      d->attn_src = LnSource{};
-      d->attn_src.emb = reinterpret_cast<const _Float16*>(d->emb.p);
-      d->attn_src.tok = d->tokens.p;
-      d->attn_src.V = d->V;
-    }
+    R.oacc = d->oacc_run.p, R.oproj_out = R.o;
   }
   return d->layer_attn(layer, st, R);
 }

@@ -309,16 +309,6 @@ bool oproj_fuse_on() {
   return true;
 #endif
 }
-// The FP16 decoder's LayerNorm + q/k/v projection + KV append fused into the
-// same workgroups (decoder.cpp): tuning build only (LLM_QKV_FUSE=1), since
-// same-box it lost C2 -6.6 % against the q/k/v GEMM launch.
-bool qkv_fuse_on() {
-#if LLM_TUNING
-  return env_int("LLM_QKV_FUSE", 0) != 0;
-#else
-  return false;
-#endif
-}
 namespace {
 int beam_mfma_balance16() {
 #if LLM_TUNING
@@ -347,19 +337,6 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
   constexpr int ST = split_stages<D, TS, LLM_F16>();
   if (a.wgm) {  // pa_decode_internal: group 1, 2..8 splits, not direct
     if constexpr (D <= kOprojMaxD) {
-#if LLM_TUNING
-      if (a.o_acc && a.qkv_w) {  // + the fused LayerNorm / q, k, v projection / KV append
-        if (a.H * D <= 1024)
-          hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
-                                              LLM_F16, true, true, true, 4>),
-                             dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
-        else
-          hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
-                                              LLM_F16, true, true, true, 8>),
-                             dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
-        return hipGetLastError();
-      }
-#endif
       if (a.o_acc) {
         hipLaunchKernelGGL((pa_split_kernel<D, TS, false, 16384, kKvLoadAux, ST, 0, false, false,
                                             LLM_F16, true, true, true>),
@@ -681,14 +658,6 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                          D <= kOprojMaxD && H <= 64),
               "pa_decode: fused o_proj needs W_o head slices, an output, a range flag, o_n > 0, "
               "head_dim <= 128 and at most 64 heads");
-  // + the fused LayerNorm / q, k, v projection (PaRowOutputs::qkv_w)
-  const bool qkv = oproj && rows->qkv_w;
-  LLM_REQUIRE(!qkv || LLM_TUNING, "pa_decode: the fused q/k/v projection is a tuning-build form");
-  LLM_REQUIRE(!qkv || ((rows->ln_x || (rows->ln_emb && rows->ln_tok && rows->ln_V > 0)) &&
-                       rows->ln_g && rows->ln_b && (H * D) % 8 == 0 && H * D <= kQkvMaxHid &&
-                       context_lens),
-              "pa_decode: the fused q/k/v projection needs the LayerNorm input and parameters, "
-              "context lengths, hidden size a multiple of 8 and <= 2048");
   LLM_REQUIRE(!rows || !rows->q || rows->inv_scale, "pa_decode: row quantisation needs inv_scale");
   LLM_REQUIRE(!row_out || (size_t)H * D * 4 <= 65536, "pa_decode: row outputs need H*D <= 16384");
   LLM_REQUIRE(!rows || !rows->pack || (H * D) % 64 == 0, "pa_decode: packed row outputs need H*D % 64 == 0");
@@ -786,8 +755,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     plan->nsplit = nsplit;
     plan->form = (direct ? LLM_PA_FORM_DIRECT : wg ? LLM_PA_FORM_WG_MERGE
                   : row_out ? LLM_PA_FORM_SPLIT_MERGE_ROW : LLM_PA_FORM_SPLIT_MERGE) |
-                 (beam ? LLM_PA_FORM_BEAM : 0) | (oproj && wg ? LLM_PA_FORM_OPROJ : 0) |
-                 (qkv && wg ? LLM_PA_FORM_QKV : 0);
+                 (beam ? LLM_PA_FORM_BEAM : 0) | (oproj && wg ? LLM_PA_FORM_OPROJ : 0);
     return LLM_OK;
   }
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
@@ -835,17 +803,6 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
       a.wo_heads = static_cast<const _Float16*>(rows->wo_heads);
       a.o_n = rows->o_n;
       a.o_flag = rows->o_flag;
-      if (qkv) {
-        a.qkv_w = static_cast<const _Float16*>(rows->qkv_w);
-        a.ln_x = rows->ln_x;
-        a.ln_emb = static_cast<const _Float16*>(rows->ln_emb);
-        a.ln_tok = rows->ln_tok;
-        a.ln_V = rows->ln_V;
-        a.ln_g = rows->ln_g;
-        a.ln_b = rows->ln_b;
-        a.ln_eps = rows->ln_eps;
-        a.ln_tap = static_cast<_Float16*>(rows->ln_tap);
-      }
     }
   }
   hipError_t e;

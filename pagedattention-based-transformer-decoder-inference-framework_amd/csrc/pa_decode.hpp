@@ -36,21 +36,6 @@ struct PaRowOutputs {
   // device int set to 1 when a head's term left the accumulator's range and was
   // clamped (common.hpp oacc_term); required with o_acc
   int* o_flag = nullptr;
-  // FP16 decoder, fused LayerNorm + q/k/v projection (with o_acc; form
-  // LLM_PA_FORM_QKV): each (row, head) workgroup normalises its row (ln_x,
-  // or E[ln_tok[b]] when ln_emb is set) with ln_g / ln_b, projects its head's
-  // q, k, v with qkv_w ([H][hid/8][3D][8] fp16), appends k, v to the page of
-  // position context_lens[b] - 1 and attends; q (the `q` argument) is unused.
-  // ln_tap (optional): the LN1 rows in packed-A order (activation taps).
-  const void* qkv_w = nullptr;
-  const float* ln_x = nullptr;
-  const void* ln_emb = nullptr;
-  const int32_t* ln_tok = nullptr;
-  int ln_V = 0;
-  const float* ln_g = nullptr;
-  const float* ln_b = nullptr;
-  float ln_eps = 1e-5f;
-  void* ln_tap = nullptr;
 };
 
 // The launch a call takes (pa_decode_plan): splits per (row, head) and
@@ -72,9 +57,6 @@ int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 // Whether the FP16 decoder fuses its o_proj into the attention's workgroup
 // merge (PaRowOutputs::o_acc); always in the product build.
 bool oproj_fuse_on();
-// Whether it also fuses LN1 + the q/k/v projection + the KV append into the
-// same workgroups (PaRowOutputs::qkv_w); always in the product build.
-bool qkv_fuse_on();
 
 // Split merge of per-(row, head, split) partial softmax states into rows
 // (out fp32 [B][H*D] and/or the rows->q / out16 o_proj inputs); row b's

@@ -88,27 +88,11 @@ struct PaSplitArgs {
   const _Float16* wo_heads;  // [H][D/8][o_n][8]
   int o_n;
   int* o_flag;  // set to 1 when a head's term was clamped (common.hpp oacc_term)
-  // WGM + OPROJ, fused LayerNorm + q/k/v projection (QKV, PaRowOutputs::qkv_w):
-  // the (b, h) workgroup computes LN1 of row b (ln_x, or the token embedding
-  // row E[ln_tok[b]] at layer 0) and its head's q, k, v itself, appends k, v
-  // to the page of position context_lens[b] - 1, runs its splits over the
-  // context before that token and adds the new token's own state in the merge
-  const float* ln_x;        // [B][hid] fp32
-  const _Float16* ln_emb;   // or E rows (fp16 [ln_V][hid])
-  const int32_t* ln_tok;
-  int ln_V;
-  const float* ln_g;
-  const float* ln_b;
-  float ln_eps;
-  const _Float16* qkv_w;    // [H][hid/8][3D][8]: column c = q (c < D), k (< 2D), v
-  _Float16* ln_tap;         // optional: LN1 rows in packed-A order (taps), head 0 writes
   // tuning (pa_split_kernel STAMPS): per wave wid, s_memrealtime (100 MHz) at
   // entry, at the first KV load, after the shared-prefix chunks, at exit, and
   // the wave's HW_ID (CU / SIMD / XCC placement): stamps[wid * 5 + 0..4]
   unsigned long long* stamps;
 };
-
-constexpr int kQkvMaxHid = 2048;  // fused q/k/v: the LN1 row in LDS as fp16
 
 constexpr int kWgmMaxSplits = 8;  // one merge batch (pa_merge_row_kernel's kMergeBatch)
 constexpr int kOprojMaxD = 128;   // fused o_proj: two W_o column slices of D fp16 in VGPRs
@@ -163,111 +147,6 @@ constexpr bool kv_shape_ok(int D, int TS, int es) {
 // (scripts/tune_attention.py, variants 0 vs 1).
 constexpr int kKvLoadAux = 2;
 
-// The fused LayerNorm + q/k/v projection of one (row b, head h) workgroup
-// (PaSplitArgs::qkv_w; decoder/decoder_block.hpp:43-55, the q/k/v GEMM of
-// the FP16 decoder with its LN1 prologue, and the KV append of
-// KVTileCache::get_write_ptr, kv_cache/kv_tile_cache.hpp:28-34).  Wave 0
-// normalises the row (ln_wave.hpp: the GEMM prologue's arithmetic, rounded to
-// fp16 as the GEMM's A); every thread then owns columns t, t + 64 nsplit, ...
-// of the head's 3D q/k/v columns: fp16 products summed in fp32 (v_dot2),
-// weights [h][hid/8][3D][8] so one load instruction reads 1 KiB contiguous,
-// two batches of 16 loads in flight (the first issued before the LayerNorm).
-// q (fp32) and k, v (fp16-rounded) land in qkv_lds; k, v also go to the
-// page of position pos.  Ends with a workgroup barrier.
-template <int D, int TS, int CPL>
-__device__ __forceinline__ void qkv_prologue(const PaSplitArgs& a, int b, int h, int r, int pos,
-                                             float (*qkv_lds)[D]) {
-  __shared__ __attribute__((aligned(16))) _Float16 ln_lds[kQkvMaxHid];
-  constexpr int BK = 16;
-  const int lane = lane_id();
-  const int w = wave_id_uniform();
-  const int nthr = 64 * a.nsplit;
-  const int hid = a.H * D;
-  const int KG = hid >> 3;
-  constexpr int NC = 3 * D;
-  const f16x8* wbase = reinterpret_cast<const f16x8*>(a.qkv_w) + (size_t)h * KG * NC;
-  f16x8 w0[BK], w1[BK];
-  auto issue = [&](f16x8 (&wb)[BK], int col, int kg0) {
-#pragma unroll
-    for (int i = 0; i < BK; ++i) {
-      const int kg = kg0 + i;
-      wb[i] = kg < KG ? wbase[(size_t)min(kg, KG - 1) * NC + col] : f16x8{};
-    }
-  };
-  const f16x2* lp = reinterpret_cast<const f16x2*>(ln_lds);
-  float acc[4];
-  auto dots = [&](const f16x8 (&wb)[BK], int kg0) {
-#pragma unroll
-    for (int i = 0; i < BK; ++i) {
-      const int kg = kg0 + i;
-      if (kg < KG) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          acc[e] = __builtin_amdgcn_fdot2(f16x2{wb[i][2 * e], wb[i][2 * e + 1]}, lp[4 * kg + e],
-                                          acc[e], false);
-      }
-    }
-  };
-  int col = threadIdx.x;
-  if (col < NC) {
-    issue(w0, col, 0);
-    issue(w1, col, BK);
-  }
-  if (w == 0) {
-    LnRow<CPL> x, gm, bt;
-    const int K4 = hid >> 2;
-    if (a.ln_emb)
-      ln_wave_load_f16<CPL>(ln_embed_row(a.ln_emb, a.ln_tok, b, a.ln_V, hid), K4, true, x);
-    else
-      ln_wave_load<CPL>(a.ln_x + (size_t)b * hid, K4, true, x);
-    ln_wave_load<CPL>(a.ln_g, K4, true, gm);
-    ln_wave_load<CPL>(a.ln_b, K4, true, bt);
-    ln_wave_compute<CPL>(x, gm, bt, hid, a.ln_eps);
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-      const int c = 64 * j + lane;
-      if (c < K4) {
-        const ln_f16x4 y = ln_half4(x.v[j]);
-        *reinterpret_cast<ln_f16x4*>(ln_lds + 4 * c) = y;
-        if (a.ln_tap && h == 0)  // the taps read the LN1 rows as the GEMM's packed A
-          *reinterpret_cast<ln_f16x4*>(a.ln_tap + a_frag_off_f16(b, 4 * c, hid >> 5)) = y;
-      }
-    }
-  }
-  __syncthreads();
-  for (; col < NC; col += nthr) {
-    if (col != (int)threadIdx.x) {
-      issue(w0, col, 0);
-      issue(w1, col, BK);
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc[e] = 0.f;
-    for (int kg0 = 0; kg0 < KG; kg0 += 2 * BK) {
-      dots(w0, kg0);
-      if (kg0 + 2 * BK < KG) issue(w0, col, kg0 + 2 * BK);
-      dots(w1, kg0 + BK);
-      if (kg0 + 3 * BK < KG) issue(w1, col, kg0 + 3 * BK);
-    }
-    const float y = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    const int which = col / D, d = col % D;
-    if (which == 0) {
-      qkv_lds[0][d] = y;
-    } else {
-      const _Float16 hy = (_Float16)y;
-      qkv_lds[which][d] = (float)hy;
-      if (pos >= 0 && r >= 0 && r < a.num_beams && pos / TS < a.max_tiles) {
-        const int page = a.page_table[((size_t)r * a.H + h) * a.max_tiles + pos / TS];
-        if (page >= 0 && page < a.num_pages) {
-          uint8_t* pool = const_cast<uint8_t*>(which == 1 ? a.k_pool : a.v_pool);
-          *reinterpret_cast<_Float16*>(pool + (size_t)page * a.page_stride +
-                                       ((size_t)(pos % TS) * D + d) * 2) = hy;
-        }
-      }
-    }
-  }
-  __syncthreads();
-}
-
 // STAGES = register stages in flight per wave (2: the next chunk loads while
 // the current one is computed; 1: latency hidden by occupancy alone).
 // MIN_WAVES > 0 asks the compiler for that many waves per SIMD.
@@ -285,7 +164,7 @@ __device__ __forceinline__ void qkv_prologue(const PaSplitArgs& a, int b, int h,
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int QKV = 0, int RING = 0, bool STAMPS = false>
+          int RING = 0, bool STAMPS = false>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -301,7 +180,6 @@ void pa_split_kernel(PaSplitArgs a) {
 
   static_assert(!(WGM && (DIRECT || BEAM)), "the workgroup merge is a split form");
   static_assert(!OPROJ || (WGM && KVT == LLM_F16), "the fused o_proj is a workgroup-merge form");
-  static_assert(QKV == 0 || OPROJ, "the fused q/k/v projection is an o_proj-fused form");
   const unsigned long long t_entry = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int lane = lane_id();
   const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
@@ -339,13 +217,6 @@ void pa_split_kernel(PaSplitArgs a) {
   const int r = a.beam_ids ? a.beam_ids[b] : b;
   int Tb = a.context_lens ? a.context_lens[b] : a.T;
   Tb = min(max(Tb, 0), a.T);
-  // QKV: this workgroup projects the new token (position Tb - 1) itself; its
-  // splits attend positions < Tb - 1 and the merge adds the token's own state
-  __shared__ __attribute__((aligned(16))) float qkv_lds[QKV ? 3 : 1][QKV ? D : 1];
-  if constexpr (QKV != 0) {
-    qkv_prologue<D, TS, QKV>(a, b, h, r, Tb - 1, qkv_lds);
-    Tb = max(Tb - 1, 0);
-  }
   const int ntiles = min((Tb + TS - 1) / TS, a.max_tiles);
   int tile0, count;
   {
@@ -480,10 +351,7 @@ void pa_split_kernel(PaSplitArgs a) {
 
   // q chunk of this lane (dims c*EPL .. c*EPL+EPL-1), pre-scaled into log2 units.
   float qv[EPL];
-  if constexpr (QKV != 0) {
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) qv[e] = qkv_lds[0][c * EPL + e] * a.qscale;
-  } else {
+  {
     const float* qp = a.q + (size_t)b * a.q_stride + (size_t)h * D + c * EPL;
 #pragma unroll
     for (int e0 = 0; e0 < EPL; e0 += 4) {
@@ -795,20 +663,11 @@ void pa_split_kernel(PaSplitArgs a) {
       const int ns = min(a.nsplit, (ntiles + pps - 1) / pps);
       const float m0 = lane < ns ? wg_ml[lane][0] : kNegSentinel;
       const float l0 = lane < ns ? wg_ml[lane][1] : 0.f;
-      // QKV: the new token's score (log2 units) from this workgroup's own q, k
-      float snew = kNegSentinel;
-      if constexpr (QKV != 0) {
-        float t = 0.f;
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) t = fmaf(qv[e], qkv_lds[1][c * EPL + e], t);
-        snew = group_sum<LPT>(t);
-      }
-      float M = ln_wave_max(fmaxf(m0, kNegSentinel));
-      if constexpr (QKV != 0) M = fmaxf(M, snew);
+      const float M = ln_wave_max(fmaxf(m0, kNegSentinel));
       float o[EPL];
 #pragma unroll
       for (int e = 0; e < EPL; ++e) o[e] = 0.f;
-      if ((ns > 0 || QKV != 0) && M > 0.5f * kNegSentinel) {
+      if (ns > 0 && M > 0.5f * kNegSentinel) {
         const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
         float L = 0.f;
 #pragma unroll
@@ -818,8 +677,6 @@ void pa_split_kernel(PaSplitArgs a) {
             const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
             L += ls * ws;
           }
-        const float wn = QKV != 0 ? __builtin_amdgcn_exp2f(snew - M) : 0.f;
-        if constexpr (QKV != 0) L += wn;  // the new token after the splits
         const float inv = 1.0f / (L + 1e-6f);
         float am[EPL];
 #pragma unroll
@@ -830,10 +687,6 @@ void pa_split_kernel(PaSplitArgs a) {
           const float* src = &wg_acc[min(s2, max(ns - 1, 0))][c * EPL];
 #pragma unroll
           for (int e = 0; e < EPL; ++e) am[e] += src[e] * ws;
-        }
-        if constexpr (QKV != 0) {
-#pragma unroll
-          for (int e = 0; e < EPL; ++e) am[e] += qkv_lds[2][c * EPL + e] * wn;
         }
 #pragma unroll
         for (int e = 0; e < EPL; ++e) o[e] = am[e] * inv;

@@ -671,275 +671,6 @@ __global__ __launch_bounds__(256) void pa_beam_mfma_kernel(PaSplitArgs a) {
   }
 }
 
-// MQ (tuning build, LLM_BEAM4=2): pa_beam4_kernel's schedule -- one wave per
-// (group of 4 beams, head, split), every page item loaded ONCE into registers,
-// no LDS staging, no barrier -- with the 4 beams' q.k on the matrix cores:
-// per page 4 + 4 v_mfma_f32_16x16x32_f16 (A = the 4 beams' q rows as fp16 hi
-// and residual lo scaled by 2^13, B = K^T loaded straight in B-operand order:
-// lane l reads token l & 15, dims 32 c + 8 (l >> 4) .. + 7), so the scores of
-// beam r for token t land in lane t, register r (lanes 0..15).  Online
-// softmax per beam over the page's 16 tokens (DPP within lanes 0..15; m and l
-// wave-uniform), p of the 4 beams per token through 256 B of the wave's LDS,
-// p.v on VALU (one fma per element and beam, V in its natural layout: lane L
-// holds token 4 i + (L >> 4), dims 8 (L & 15) .. + 7).  The VALU form spends
-// 4 waves x ~120 instructions per shared page; this form ~180 for all 4.
-// D 128, page 16, fp16 only.  STAGES: pages in flight per wave (2: the next
-// page loads while the current one is computed; 1: latency hidden by the
-// third wave per SIMD the freed registers allow, MINW 3).
-template <int MINW = 2, int STAGES = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void pa_beam_mq_kernel(PaSplitArgs a) {
-  constexpr int D = 128, TS = 16, G = 4;
-  constexpr int PAGE_BYTES = TS * D * 2;
-  __shared__ __attribute__((aligned(16))) f32x4 p_lds[4][TS];
-  const int lane = lane_id();
-  const int wv = wave_id_uniform();
-  const int wid = blockIdx.x * 4 + wv;
-  const int s = wid % a.nsplit;
-  const int gh = wid / a.nsplit;
-  const int h = gh % a.H;
-  const int grp = gh / a.H;
-  if (grp >= (a.B + G - 1) / G) return;
-  const int b0 = grp * G;
-
-  int prow_off[G], Tg[G];
-  bool live[G];
-  bool share = true;
-#pragma unroll
-  for (int i = 0; i < G; ++i) {
-    const int bi = b0 + i;
-    live[i] = bi < a.B;
-    int ri = -1, Ti = 0;
-    if (live[i]) {
-      ri = a.beam_ids ? a.beam_ids[bi] : bi;
-      Ti = a.context_lens ? a.context_lens[bi] : a.T;
-      Ti = min(max(Ti, 0), a.T);
-    }
-    const bool rok = ri >= 0 && ri < a.num_beams;
-    prow_off[i] = rok ? (ri * a.H + h) * a.max_tiles : -1;
-    Tg[i] = rok ? Ti : 0;
-    if (!live[i] || !rok || Ti != Tg[0]) share = false;
-  }
-
-  // A operands: row r = lane & 15 (r < 4: beam r), k = 32 c + 8 (lane >> 4) .. + 7
-  f16x8 qh[4], ql[4];
-  {
-    const int r = lane & 15;
-    const bool qok = r < G && b0 + r < a.B;
-    const float* qp = a.q + (size_t)(qok ? b0 + r : 0) * a.q_stride + (size_t)h * D;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = qok ? qp[32 * c + 8 * (lane >> 4) + e] * a.qscale : 0.f;
-        const _Float16 hi = fabsf(v) >= kF16MinNormal ? (_Float16)v : (_Float16)0.f;
-        qh[c][e] = hi;
-        ql[c][e] = (_Float16)((v - (float)hi) * kLoScale);
-      }
-  }
-  float m[G], l[G], acc[G][8];
-#pragma unroll
-  for (int i = 0; i < G; ++i) {
-    m[i] = kNegSentinel;
-    l[i] = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[i][e] = 0.f;
-  }
-  // K in B-operand order (token l & 15, 16 B at dims 32 c + 8 (l >> 4)); V linear
-  const uint32_t k_off = (uint32_t)((lane & 15) * (D * 2) + 16 * (lane >> 4));
-  const uint32_t v_off = (uint32_t)lane * 16u;
-
-  const int nseg = share ? 1 : G;
-  for (int seg = 0; seg < nseg; ++seg) {
-    int i0 = 0, cnt = 0, nsh = 0, ntiles = 0;
-    if (share) {
-      ntiles = min((Tg[0] + TS - 1) / TS, a.max_tiles);
-      // the shared prefix: the page ids of the first 512 tiles of all 4 rows in
-      // one round trip, then 64-tile rounds past them
-      int idv[8][G];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const int t = 64 * k + lane;
-          idv[k][i] = t < ntiles ? a.page_table[prow_off[i] + t] : -1;
-        }
-      bool done = false;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // (k static: idv stays in registers)
-        const int t = 64 * k + lane;
-        if (!done && 64 * k < ntiles) {
-          bool eq = t < ntiles;
-#pragma unroll
-          for (int i = 1; i < G; ++i) eq = eq && idv[k][i] == idv[k][0];
-          const uint64_t mk = __ballot(eq);
-          const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
-          nsh = 64 * k + run;
-          done = run < 64;
-        }
-      }
-      if (nsh >= 512) {
-        for (int blk = 512; blk < ntiles; blk += 64) {
-          const int t = blk + lane;
-          bool eq = t < ntiles;
-          if (eq) {
-            const int32_t p0 = a.page_table[prow_off[0] + t];
-#pragma unroll
-            for (int i = 1; i < G; ++i) eq = eq && a.page_table[prow_off[i] + t] == p0;
-          }
-          const uint64_t mk = __ballot(eq);
-          const int run = mk == ~0ull ? 64 : __builtin_ctzll(~mk);
-          nsh = blk + run;
-          if (run < 64) break;
-        }
-      }
-      nsh = min(nsh, ntiles);
-      const int items = nsh + G * (ntiles - nsh);
-      i0 = (int)(((long long)items * s) / a.nsplit);
-      cnt = (int)(((long long)items * (s + 1)) / a.nsplit) - i0;
-    } else {
-      if (prow_off[seg] < 0) continue;
-      ntiles = min((Tg[seg] + TS - 1) / TS, a.max_tiles);
-      const int pps = row_pps(0, a.nsplit, ntiles);
-      i0 = s * pps;
-      cnt = min(pps, ntiles - i0);
-    }
-    cnt = min(cnt, kMaxPps);
-    if (cnt <= 0) continue;
-    const int npriv = ntiles - nsh;
-    int pid[2], inf[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int j = lane + 64 * r;
-      pid[r] = -1;
-      inf[r] = 0;
-      if (j < cnt) {
-        const int k = i0 + j;
-        int tile, beam, mask;
-        if (!share) {
-          tile = k; beam = seg; mask = 1 << seg;
-        } else if (k < nsh) {
-          tile = k; beam = 0; mask = 0xF;
-        } else {
-          const int p = k - nsh;
-          beam = p / npriv; tile = nsh + p % npriv; mask = 1 << beam;
-        }
-        const int id = a.page_table[prow_off[beam] + tile];
-        pid[r] = id >= a.num_pages ? -1 : id;
-        inf[r] = (tile << 4) | mask;
-      }
-    }
-    auto item_pid = [&](int j) {
-      return j < 64 ? __builtin_amdgcn_readlane(pid[0], j) : __builtin_amdgcn_readlane(pid[1], j - 64);
-    };
-    auto item_inf = [&](int j) {
-      return j < 64 ? __builtin_amdgcn_readlane(inf[0], j) : __builtin_amdgcn_readlane(inf[1], j - 64);
-    };
-    const int Tb = share ? Tg[0] : Tg[seg];
-    auto issue = [&](u32x4 (&kk)[4], u32x4 (&vv)[4], int j) {
-      const int pg = j < cnt ? item_pid(min(j, kMaxPps - 1)) : -1;
-      const bool ok = pg >= 0;
-      const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
-      const auto krs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.k_pool + off), (short)0,
-                                                         ok ? PAGE_BYTES : 0, 0x00020000);
-      const auto vrs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.v_pool + off), (short)0,
-                                                         ok ? PAGE_BYTES : 0, 0x00020000);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        kk[c] = __builtin_amdgcn_raw_buffer_load_b128(krs, k_off + 64 * c, 0, kKvLoadAux);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        vv[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, v_off + 1024 * i, 0, kKvLoadAux);
-    };
-    auto compute = [&](const u32x4 (&kk)[4], const u32x4 (&vv)[4], int j) {
-      const int pg = item_pid(min(j, kMaxPps - 1));
-      const int info = item_inf(min(j, kMaxPps - 1));
-      const int tile = info >> 4, mask = info & 0xF;
-      const bool ok = pg >= 0;
-      const int tok0 = tile * TS;
-      const bool full = ok && tok0 + TS <= Tb;
-      f32x4 sh = f32x4{0.f, 0.f, 0.f, 0.f}, sl = sh;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const f16x8 kb = __builtin_bit_cast(f16x8, kk[c]);
-        sh = __builtin_amdgcn_mfma_f32_16x16x32_f16(qh[c], kb, sh, 0, 0, 0);
-        sl = __builtin_amdgcn_mfma_f32_16x16x32_f16(ql[c], kb, sl, 0, 0, 0);
-      }
-      // lanes 0..15: token tok0 + lane, register r: beam r
-      const bool tok_ok = lane < 16 && (full || (ok && tok0 + lane < Tb));
-      float p[G], corr[G];
-#pragma unroll
-      for (int r = 0; r < G; ++r) {
-        const bool valid = tok_ok && ((mask >> r) & 1);
-        const float sv = valid ? sh[r] + sl[r] * kLoUnscale : kNegSentinel;
-        const float mx = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(row_max16(sv))));
-        const float mnew = fmaxf(m[r], mx);
-        corr[r] = __builtin_amdgcn_exp2f(m[r] - mnew);
-        p[r] = valid ? __builtin_amdgcn_exp2f(sv - mnew) : 0.f;
-        const float ps = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(group_sum<16>(p[r]))));
-        l[r] = l[r] * corr[r] + ps;
-        m[r] = mnew;
-      }
-      if (lane < 16) p_lds[wv][lane] = f32x4{p[0], p[1], p[2], p[3]};
-      if (corr[0] != 1.f || corr[1] != 1.f || corr[2] != 1.f || corr[3] != 1.f) {  // uniform
-#pragma unroll
-        for (int r = 0; r < G; ++r)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) acc[r][e] *= corr[r];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int t = 4 * i + (lane >> 4);
-        const f32x4 pp = p_lds[wv][t];
-        const u32x4 vraw = full || (ok && tok0 + t < Tb) ? vv[i] : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int r = 0; r < G; ++r)
-          if ((mask >> r) & 1) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[r][e] = fmaf(pp[r], kv_at<LLM_F16>(vraw, e), acc[r][e]);
-          }
-      }
-    };
-    if constexpr (STAGES == 1) {
-      u32x4 kA[4], vA[4];
-      for (int j = 0; j < cnt; ++j) {
-        issue(kA, vA, j);
-        compute(kA, vA, j);
-      }
-    } else {
-      u32x4 kA[4], vA[4], kB[4], vB[4];
-      issue(kA, vA, 0);
-      for (int j = 0; j < cnt; j += 2) {
-        issue(kB, vB, j + 1);
-        compute(kA, vA, j);
-        if (j + 1 >= cnt) break;
-        issue(kA, vA, j + 2);
-        compute(kB, vB, j + 1);
-      }
-    }
-  }
-
-  // per beam: sum the 4 token groups (same m), write the split partial
-#pragma unroll
-  for (int i = 0; i < G; ++i) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      acc[i][e] += __shfl_xor(acc[i][e], 16, 64);
-      acc[i][e] += __shfl_xor(acc[i][e], 32, 64);
-    }
-    if (!live[i]) continue;
-    const size_t pidx = ((size_t)(b0 + i) * a.H + h) * a.nsplit + s;
-    if (lane < 16) {
-      float* o = a.part_acc + pidx * D + 8 * lane;
-      *reinterpret_cast<f32x4*>(o) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
-      *reinterpret_cast<f32x4*>(o + 4) = f32x4{acc[i][4], acc[i][5], acc[i][6], acc[i][7]};
-    }
-    if (lane == 0) {
-      a.part_ml[pidx * 2] = m[i];
-      a.part_ml[pidx * 2 + 1] = l[i];
-    }
-  }
-}
-
 #ifndef BEAM4_MINW
 #define BEAM4_MINW 2
 #endif
@@ -969,30 +700,8 @@ long long beam4_resident_waves() {
   }
 }
 
-static int beam4_mode() { return env_int("LLM_BEAM4", 0); }  // read per launch
-
-// LLM_BEAM4 = 2: pa_beam_mq_kernel<2, 2>; 3: <3, 1> (one page in flight, 3 waves per SIMD)
-template <int MINW, int STAGES>
-long long beam_mq_resident_waves() {
-  static long long cached = 0;
-  if (cached) return cached;
-  int dev = 0, cus = 0, blocks = 0;
-  if (hipGetDevice(&dev) == hipSuccess &&
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, pa_beam_mq_kernel<MINW, STAGES>, 256, 0) ==
-          hipSuccess &&
-      cus > 0 && blocks > 0) {
-    cached = (long long)cus * blocks * 4;
-  } else {
-    (void)hipGetLastError();
-    cached = 256LL * 4 * 2;
-  }
-  return cached;
-}
 
 long long tune_beam4_resident_for(int D, int TS) {
-  if (beam4_mode() == 2 && D == 128 && TS == 16) return beam_mq_resident_waves<2, 2>();
-  if (beam4_mode() == 3 && D == 128 && TS == 16) return beam_mq_resident_waves<3, 1>();
   auto by_ts = [&](auto d) -> long long {
     constexpr int DD = decltype(d)::value;
     return TS == 16 ? beam4_resident_waves<DD, 16>() : beam4_resident_waves<DD, 32>();
@@ -1008,14 +717,6 @@ long long tune_beam4_resident_for(int D, int TS) {
 hipError_t tune_launch_beam4(const PaSplitArgs& a, int D, int TS, hipStream_t st) {
   const int waves4 = ((a.B + 3) / 4) * a.H * a.nsplit;
   const dim3 grid((waves4 + 3) / 4), block(256);
-  if (beam4_mode() == 2 && D == 128 && TS == 16) {
-    hipLaunchKernelGGL((pa_beam_mq_kernel<2, 2>), grid, block, 0, st, a);
-    return hipGetLastError();
-  }
-  if (beam4_mode() == 3 && D == 128 && TS == 16) {
-    hipLaunchKernelGGL((pa_beam_mq_kernel<3, 1>), grid, block, 0, st, a);
-    return hipGetLastError();
-  }
   auto go = [&](auto d, auto ts) {
     constexpr int DD = decltype(d)::value, TT = decltype(ts)::value;
     if constexpr (TT * DD * 2 <= 8192)
@@ -1064,7 +765,7 @@ hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st
     constexpr int R = decltype(r)::value;
     constexpr bool LO = decltype(lo)::value;
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, LO, true, LLM_F16,
-                                        true, false, false, 0, R>),
+                                        true, false, false, R>),
                        grid, dim3(256), 0, st, a);
   };
   auto by_ring = [&](auto lo) {
@@ -1102,7 +803,7 @@ hipError_t tune_launch_beam_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t
   a.stamps = g_stamps;
   g_stamps_waves = waves;
   hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
-                                      true, false, false, 0, 0, true>),
+                                      true, false, false, 0, true>),
                      grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -37,7 +37,6 @@ LOGIT_TOL = 1e-3
 TIE_TOL = 1e-5
 FORM_DIRECT, FORM_SPLIT_MERGE, FORM_SPLIT_MERGE_ROW, FORM_WG_MERGE, FORM_BEAM = 0, 1, 2, 3, 16
 FORM_OPROJ = 32  # FP16 decoder: o_proj fused into the workgroup merge
-FORM_QKV = 64    # ... and LN1 + q/k/v + KV append in the same workgroups (tuning build)
 
 
 def _torch():

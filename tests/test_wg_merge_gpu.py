@@ -46,12 +46,10 @@ def _model(rng, L, H, D, V):
     return {k: np.ascontiguousarray(v) for k, v in w.items()}
 
 
-def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16, fuse=True, taps=False,
-         qkv=False):
+def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16, fuse=True, taps=False):
     """Logits of `steps` decode steps of a fresh FP16 decoder of `lib`
     (tuning build: splits > 0 forces the split count, fuse=False keeps the
-    o_proj GEMM launch instead of the workgroup merge's fused o_proj, qkv=True
-    the fused LN1 + q/k/v projection instead of the q/k/v GEMM launch).
+    o_proj GEMM launch instead of the workgroup merge's fused o_proj).
     taps=True: also the activation taps of the last step (llm_decoder_set_taps:
     per layer the four packed fp16 GEMM inputs), as uint16 [L][4][B16 * qa_ld]."""
     import torch
@@ -59,7 +57,6 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16, fuse=True, 
     os.environ["LLM_WG_MERGE"] = "1" if wgm else "0"
     os.environ["LLM_WGM_SPLITS"] = str(splits)
     os.environ["LLM_OPROJ_FUSE"] = "1" if fuse else "0"
-    os.environ["LLM_QKV_FUSE"] = "1" if qkv else "0"
     lib.llm_decoder_create.argtypes = [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_void_p)]
     lib.llm_decoder_set_f16_weights.argtypes = [ctypes.c_void_p, ctypes.POINTER(_F16W)]
     lib.llm_decoder_begin_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -100,7 +97,6 @@ def _run(lib, w, L, H, D, V, S, B, ctx, steps, wgm, splits=0, ts=16, fuse=True, 
         os.environ.pop("LLM_WG_MERGE", None)
         os.environ.pop("LLM_WGM_SPLITS", None)
         os.environ.pop("LLM_OPROJ_FUSE", None)
-        os.environ.pop("LLM_QKV_FUSE", None)
 
 
 @pytest.mark.parametrize("H,D,ts", [(12, 64, 16), (8, 128, 16), (4, 256, 16), (8, 128, 32)],
@@ -148,8 +144,8 @@ def test_fused_oproj(gpu, ctx, H, D, ts):
     L, V, S, B = 2, 512, 2100, 16
     w = _model(np.random.default_rng(4), L, H, D, V)
     for ns in (3, 8):
-        fused = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True, qkv=False)
-        again = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True, qkv=False)
+        fused = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True)
+        again = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True)
         gemm = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=False)
         assert np.isfinite(fused).all()
         assert np.array_equal(fused.view(np.uint32), again.view(np.uint32)), ns
@@ -159,8 +155,7 @@ def test_fused_oproj(gpu, ctx, H, D, ts):
         # the same bits, and fc1's input LN2(x) -- x the o_proj output, rounded
         # to fp16 -- differs in a few elements by one fp16 ulp (or, where
         # x - mean cancels, by 1e-5 of the tensor's largest value)
-        _, tf = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True,
-                     qkv=False)
+        _, tf = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True)
         _, tg = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=False, taps=True)
         hid = H * D
         n16 = (B + 15) // 16 * 16 * hid
@@ -181,7 +176,6 @@ def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3):
     import llm_capi
     os.environ["LLM_WGM_SPLITS"] = str(splits)
     os.environ["LLM_OPROJ_FUSE"] = "1" if fuse else "0"
-    os.environ["LLM_QKV_FUSE"] = "0"  # the o_proj fusion alone (test_fused_qkv covers q/k/v)
     for name, args in (("llm_decoder_create", [ctypes.POINTER(_Cfg), ctypes.POINTER(ctypes.c_void_p)]),
                        ("llm_decoder_set_f16_weights", [ctypes.c_void_p, ctypes.POINTER(_F16W)]),
                        ("llm_decoder_begin_synthetic", [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -223,7 +217,6 @@ def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3):
         lib.llm_decoder_destroy(dec)
         os.environ.pop("LLM_WGM_SPLITS", None)
         os.environ.pop("LLM_OPROJ_FUSE", None)
-        os.environ.pop("LLM_QKV_FUSE", None)
 
 
 def test_fused_oproj_range_guard(gpu):
@@ -281,49 +274,3 @@ def test_fused_oproj_range_guard(gpu):
     wn = {k: np.ascontiguousarray(v) for k, v in wn.items()}
     _, frc, fst, _ = _guard_run(tune, wn, L, H, D, V, B, 2, fuse=True)
     assert frc == [llm_capi.LLM_ERR_RANGE] * 2 and fst == (1, 0), (frc, fst)
-
-
-@pytest.mark.parametrize("H,D,ts", [(12, 64, 16), (8, 128, 16), (8, 128, 32)],
-                         ids=["c2_width_d64", "d128", "d128_page32"])
-@pytest.mark.parametrize("ctx", [1500, 40, 0])
-def test_fused_qkv(gpu, ctx, H, D, ts):
-    """LN1 + the q/k/v projection + the KV append inside the attention's
-    workgroups (LLM_PA_FORM_QKV: each (row, head) workgroup normalises its row
-    as the GEMM's LayerNorm prologue does, projects its head's q, k, v with
-    fp16 products summed in fp32, writes k, v into the page of its position,
-    attends the context before it and adds the new token's own state in the
-    merge) against the q/k/v GEMM launch, both with the fused o_proj.  A
-    tuning-build form (LLM_QKV_FUSE=1): same-box it lost C2 -6.6 % against
-    the GEMM launch, so the product keeps the launch.  The LN1
-    rows (tapped GEMM input) the same bits; the attention rows (o_proj input)
-    within one fp16 ulp (q / k / v differ in the fp32 summation order only);
-    step logits within 3e-3 over 4 steps (1.6e-3 measured at C2's width: the
-    one-ulp o_proj inputs carried through 2 layers); bit-identical from run to
-    run; the product library (no fused form) equals the tuning build with the
-    switch off.  ctx 0: the first token attends only itself."""
-    import llm_capi
-    from _util import rel_err
-    tune = llm_capi.load_tune()
-    L, V, S, B = 2, 512, 2100, 16
-    w = _model(np.random.default_rng(6), L, H, D, V)
-    hid = H * D
-    n16 = (B + 15) // 16 * 16 * hid
-    for ns in (3, 8):
-        fq = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True, qkv=True)
-        again = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True, qkv=True)
-        gq = _run(tune, w, L, H, D, V, S, B, ctx, 4, True, ns, ts, fuse=True, qkv=False)
-        assert np.isfinite(fq).all()
-        assert np.array_equal(fq.view(np.uint32), again.view(np.uint32)), ns
-        for st in range(4):
-            assert rel_err(fq[st], gq[st]) < 3e-3, (ns, st, rel_err(fq[st], gq[st]))
-        assert not np.array_equal(fq.view(np.uint32), gq.view(np.uint32))  # the fused form ran
-        _, tf = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True, qkv=True)
-        _, tg = _run(tune, w, L, H, D, V, S, B, ctx, 1, True, ns, ts, fuse=True, taps=True, qkv=False)
-        assert np.array_equal(tf[0, 0, :n16], tg[0, 0, :n16])  # LN1 rows: the same bits
-        fa = tf[0, 1, :n16].view(np.float16).astype(np.float64)
-        fg = tg[0, 1, :n16].view(np.float16).astype(np.float64)
-        bound = np.spacing(np.abs(fg).astype(np.float16)).astype(np.float64) + 1e-5 * np.abs(fg).max()
-        assert np.all(np.abs(fa - fg) <= bound), np.max(np.abs(fa - fg) / bound)
-    prod = _run(llm_capi.load(), w, L, H, D, V, S, B, ctx, 3, True, 0, ts)
-    auto = _run(tune, w, L, H, D, V, S, B, ctx, 3, True, 0, ts)
-    assert np.array_equal(prod.view(np.uint32), auto.view(np.uint32))
