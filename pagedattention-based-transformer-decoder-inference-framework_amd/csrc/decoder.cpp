@@ -98,6 +98,9 @@ struct llm_decoder {
   DevBuf<long long> oacc, oacc_run;
   DevBuf<int> oflag;
   int* h_oflag = nullptr;
+  // beam-group attention (row_group 4): the dynamic tile counters
+  // (PaRowOutputs::beam_ctr), zero at create and left at zero by every launch
+  DevBuf<unsigned> beam_ctr;
   int oproj_range_status();
   DevBuf<int32_t> tokens, pos, ctx;
   DevBuf<uint8_t> attn_ws;
@@ -212,6 +215,8 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
     LLM_HIP_RET(hipHostMalloc(reinterpret_cast<void**>(&d->h_oflag), sizeof(int)));
     *d->h_oflag = 0;
   }
+  RET_IF(d->beam_ctr.alloc(2 * (((size_t)B + 3) / 4) * d->H));
+  LLM_HIP_RET(hipMemset(d->beam_ctr.p, 0, sizeof(unsigned) * d->beam_ctr.n));
   d->b16 = B16;
   RET_IF(d->tokens.alloc((size_t)B));
   RET_IF(d->pos.alloc((size_t)B));
@@ -528,6 +533,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
   } else {
     ro.out16 = R.act;
   }
+  if (R.row_group >= 4) ro.beam_ctr = beam_ctr.p;
   return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
                             R.row_group, plan);

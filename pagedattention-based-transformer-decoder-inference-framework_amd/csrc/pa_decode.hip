@@ -3,7 +3,7 @@
 // pa_decode_grouped, pa_decode_plan).  The split kernel itself, and the design
 // notes of the scan, are in pa_split.hpp; the tuning build's experiment
 // kernels and A/B entry are in csrc/tune/pa_decode_tune.hip.
-#include "pa_split.hpp"
+#include "pa_beam_steal.hpp"
 #if LLM_TUNING
 #include "tune/pa_decode_tune.hpp"
 #endif
@@ -309,6 +309,33 @@ bool oproj_fuse_on() {
   return true;
 #endif
 }
+// The steal form's exchange splits a shared page's 2 NI pieces of 1 KiB over
+// the 4 waves: NI = TS D / 512 even (fp16 pages of 2, 4 or 8 KiB).
+constexpr bool steal_shape_ok(int D, int TS) {
+  return D >= 8 && D <= 512 && (TS * D) % 1024 == 0 && TS * D * 2 <= 8192;
+}
+// Standalone beam launches (pa_decode C entry, no decoder-owned counters):
+// the tuning build's LLM_BEAM_STEAL=1 runs the steal form on counters of its
+// own (one buffer per process: launches must not overlap).
+unsigned* standalone_steal_counters(size_t n) {
+#if LLM_TUNING
+  static unsigned* buf = nullptr;
+  static size_t cap = 0;
+  if (env_int("LLM_BEAM_STEAL", 0) != 1) return nullptr;
+  if (n > cap) {
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipMalloc(&buf, n * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(buf, 0, n * sizeof(unsigned)) != hipSuccess) return nullptr;
+    cap = n;
+  }
+  return buf;
+#else
+  (void)n;
+  return nullptr;
+#endif
+}
 namespace {
 int beam_mfma_balance16() {
 #if LLM_TUNING
@@ -356,6 +383,13 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
     return tune_launch_beam4(a, D, TS, st);
   }
 #endif
+  if (a.group == 4 && !direct && a.steal) {  // dynamic tile assignment (pa_beam_steal.hpp)
+    if constexpr (steal_shape_ok(D, TS)) {
+      hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS>), grid, block, 0, st, a);
+      *beam = true;
+      return hipGetLastError();
+    }
+  }
   if (a.group == 4 && !direct && ST == 2) {
     // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
     // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
@@ -747,17 +781,27 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                 "pa_decode: at most 128 splits of at most 128 pages per row (raise "
                 "pages_per_split, or pass 0; T <= 16384 pages)");
   const bool direct = nsplit <= 1;
+  // beam groups of 4 fp16 rows with counters: dynamic tile assignment
+  const bool steal_form = row_group >= 4 && !direct && kv->kv_dtype == LLM_F16 &&
+                          pps_fixed <= 0 && !use_beam4 && !beam_mfma_on() &&
+                          steal_shape_ok(D, TS);
   if (plan) {
     const int group = std::max(1, std::min(row_group, 4));
     const bool wg = wgm_ok && !direct && group == 1 && nsplit <= kWgmMaxSplits;
     const bool beam = group == 4 && !direct && kv->kv_dtype == LLM_F16 &&
                       TS * D * 2 <= 8192;
+    const bool steal = steal_form && rows && rows->beam_ctr;
     plan->nsplit = nsplit;
     plan->form = (direct ? LLM_PA_FORM_DIRECT : wg ? LLM_PA_FORM_WG_MERGE
                   : row_out ? LLM_PA_FORM_SPLIT_MERGE_ROW : LLM_PA_FORM_SPLIT_MERGE) |
-                 (beam ? LLM_PA_FORM_BEAM : 0) | (oproj && wg ? LLM_PA_FORM_OPROJ : 0);
+                 (beam ? LLM_PA_FORM_BEAM : 0) | (oproj && wg ? LLM_PA_FORM_OPROJ : 0) |
+                 (steal ? LLM_PA_FORM_STEAL : 0);
     return LLM_OK;
   }
+  unsigned* steal_ctr = nullptr;
+  if (steal_form)
+    steal_ctr = rows && rows->beam_ctr ? rows->beam_ctr
+                                       : standalone_steal_counters(2 * (size_t)((B + 3) / 4) * H);
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
   if (oproj && (direct || row_group != 1 || nsplit > kWgmMaxSplits || !wgm_ok))
     return fail(LLM_ERR_UNSUPPORTED, "pa_decode: the fused o_proj needs the workgroup-merge form");
@@ -792,6 +836,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   a.balance16 = beam_balance16();
   a.beam4 = use_beam4 ? 1 : 0;
+  a.steal = a.group == 4 ? steal_ctr : nullptr;
   if (wgm) {
     a.wgm = 1;
     a.out16 = static_cast<_Float16*>(rows->out16);

@@ -36,6 +36,11 @@ struct PaRowOutputs {
   // device int set to 1 when a head's term left the accumulator's range and was
   // clamped (common.hpp oacc_term); required with o_acc
   int* o_flag = nullptr;
+  // Beam-group launches (row_group 4, fp16 KV): 2 * ceil(B / 4) * H counters,
+  // zero before the first launch and left at zero by every launch; with them
+  // the launch assigns tiles dynamically (pa_beam_steal.hpp,
+  // LLM_PA_FORM_STEAL), without them it runs the static BEAM form
+  unsigned* beam_ctr = nullptr;
 };
 
 // The launch a call takes (pa_decode_plan): splits per (row, head) and

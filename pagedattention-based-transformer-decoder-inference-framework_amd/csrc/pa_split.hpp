@@ -88,6 +88,10 @@ struct PaSplitArgs {
   const _Float16* wo_heads;  // [H][D/8][o_n][8]
   int o_n;
   int* o_flag;  // set to 1 when a head's term was clamped (common.hpp oacc_term)
+  // beam-group launches with dynamic tile assignment (pa_beam_steal.hpp):
+  // per (sequence group, head) the next-batch counter and the arrival count,
+  // zero at launch, left at zero by the launch
+  unsigned* steal;
   // tuning (pa_split_kernel STAMPS): per wave wid, s_memrealtime (100 MHz) at
   // entry, at the first KV load, after the shared-prefix chunks, at exit, and
   // the wave's HW_ID (CU / SIMD / XCC placement): stamps[wid * 5 + 0..4]

@@ -96,8 +96,9 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     shared page, and never-written (NaN) token rows past every context in both
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
     cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1),
-    its one-wave-per-group kernel (LLM_BEAM4=1) and the shipped form fed by an
-    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits)."""
+    its one-wave-per-group kernel (LLM_BEAM4=1), the shipped form fed by an
+    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits) and the decoder's
+    dynamic-assignment form (LLM_BEAM_STEAL=1)."""
     import torch
     import llm_capi
     rng = np.random.default_rng(B * 7 + T)
@@ -181,3 +182,17 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
                                   beam_ids=d(beam_ids), row_group=4,
                                   lib=llm_capi.load_tune()).cpu().numpy()
         assert np.array_equal(outr.view(np.uint32), outg.view(np.uint32)), (ring, rel_err(outr, outg))
+    monkeypatch.delenv("LLM_BEAM_RING")
+    # ... and the decoder's form: tiles assigned to the splits while the launch
+    # runs (pa_beam_steal.hpp; standalone here on the tuning build's own
+    # counters, LLM_BEAM_STEAL=1).  Run three times: the counters must come
+    # back to zero after every launch (a stale counter skips tiles).  Which
+    # split sums which tile varies run to run, so only fp32 merge rounding differs.
+    monkeypatch.setenv("LLM_BEAM_STEAL", "1")
+    for _ in range(3):
+        outs = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                                  beam_ids=d(beam_ids), row_group=4,
+                                  lib=llm_capi.load_tune()).cpu().numpy()
+        assert np.isfinite(outs).all()
+        assert_parity(outs, ref, 1e-3)
+        assert rel_err(outs, plain) < 1e-5
