@@ -11,8 +11,9 @@
 // cost-weighted split boundaries leaving a 37 -> 56 us tail in a 57 us launch
 // (exit p10 36.8 us, p90 54.9 us) and 2.3-17 us before the first KV load (the
 // 512-tile prefix scan behind beam_ids and page-table round trips).  Here:
-//   * tiles go out in batches of KB: workgroup s starts on tiles
-//     [s KB, (s + 1) KB) (no atomic before its first load), then takes the
+//   * tiles go out in batches of KB, last tile first (the beam-private tail
+//     is handed out first, the cheap shared tiles last): workgroup s starts on
+//     items [s KB, (s + 1) KB) (no atomic before its first load), then takes the
 //     next batch from a per-(sequence, head) counter (returning atomic add,
 //     issued one batch ahead, published to the other waves through LDS at
 //     mid-batch, so the next batch's page ids are in flight long before its
@@ -37,19 +38,30 @@
 
 namespace llm {
 
-constexpr int kStealBatch = 8;  // tiles per batch (4 rows x 8 ids = 32 lanes of one load)
+constexpr int kStealBatch = 4;  // tiles per batch (4 rows x KB ids: one load)
 
-template <int D, int TS>
-__global__ __launch_bounds__(256) void pa_beam_steal_kernel(PaSplitArgs a) {
+// MINW 4: 4 waves per SIMD (<= 128 VGPRs, D 128 / page 16), so the C4 grid
+// (8 splits x 8 sequences x 16 heads = 1,024 workgroups of 4 waves) is one
+// resident round; 16 KiB pages (D 256, or page 32) do not fit it and ask for 2.
+// STAMPS (tuning build): per wave wid, stamps[wid * 8 + 0..7] = s_memrealtime
+// at entry, before the first tile, after the last one, at exit; tiles
+// computed, of them shared; 10 ns ticks spent at the mid-batch barriers; HW_ID.
+template <int D, int TS, int KB = kStealBatch, int MINW = (TS * D <= 2048 ? 4 : 2),
+          bool STAMPS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MINW))) void pa_beam_steal_kernel(
+    PaSplitArgs a) {
   constexpr int EPL = 8;  // fp16
   constexpr int LPT = D / EPL;
   constexpr int TPI = 64 / LPT;
   constexpr int NI = TS / TPI;  // 1 KiB pieces per page and pool
   constexpr int PAGE_BYTES = TS * D * 2;
   constexpr int QP = NI / 2;  // pieces per wave of a shared tile (2 NI pieces over 4 waves)
-  constexpr int KB = kStealBatch;
+  static_assert(KB >= 2 && 4 * KB <= 64, "steal form: batch size");
   static_assert(LPT >= 1 && LPT <= 64 && NI >= 2 && NI % 2 == 0, "steal form: D/TS");
 
+  const unsigned long long t_entry = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  unsigned long long t_first = 0, t_last = 0, t_mid = 0;
+  int n_items = 0, n_shared = 0;
   const int lane = lane_id();
   const int gi = wave_id_uniform();  // beam within the group
   const int s = blockIdx.x % a.nsplit;
@@ -183,21 +195,26 @@ __global__ __launch_bounds__(256) void pa_beam_steal_kernel(PaSplitArgs a) {
       }
     }
   } else {
-    unsigned* ctr = a.steal + 2 * gh;  // [0] next dynamic batch (tiles past nsplit KB), [1] arrivals
+    unsigned* ctr = a.steal + 2 * gh;  // [0] next dynamic batch (items past nsplit KB), [1] arrivals
+    // items run last tile first: the beam-private tail (4 pages per tile) goes
+    // out in the static batches and the dynamic ones end on shared tiles (one
+    // page each), so the last batches taken are the cheapest
+    auto tile_of = [&](int item) { return ntiles - 1 - item; };
     __shared__ __attribute__((aligned(16))) u32x4 kvbuf[2][2 * NI][64];
     __shared__ int next_lds[2];  // by batch parity: a slot is rewritten two batches later
-    // lane j < 4 KB holds the page id of row j / KB, tile t0 + j % KB
+    // lane j < 4 KB holds the page id of row j / KB, item t0 + j % KB
     auto load_ids = [&](int t0) {
       const int j = lane;
-      const int t = t0 + j % KB;
-      return j < 4 * KB && t < ntiles ? valid_id(a.page_table[prow[min(j / KB, 3)] + t]) : -1;
+      const int it = t0 + j % KB;
+      // raw: validated after the readlane (a compare here would wait for the load)
+      return j < 4 * KB && it < ntiles ? a.page_table[prow[min(j / KB, 3)] + tile_of(it)] : -1;
     };
     // item k of a batch: shared (the page of all 4 rows) or private (this wave's own page)
     auto item_page = [&](int ids, int k, bool& shared) {
-      const int p0 = __builtin_amdgcn_readlane(ids, k);
-      const int p1 = __builtin_amdgcn_readlane(ids, KB + k);
-      const int p2 = __builtin_amdgcn_readlane(ids, 2 * KB + k);
-      const int p3 = __builtin_amdgcn_readlane(ids, 3 * KB + k);
+      const int p0 = valid_id(__builtin_amdgcn_readlane(ids, k));
+      const int p1 = valid_id(__builtin_amdgcn_readlane(ids, KB + k));
+      const int p2 = valid_id(__builtin_amdgcn_readlane(ids, 2 * KB + k));
+      const int p3 = valid_id(__builtin_amdgcn_readlane(ids, 3 * KB + k));
       shared = p0 == p1 && p0 == p2 && p0 == p3;
       return shared ? p0 : gi == 0 ? p0 : gi == 1 ? p1 : gi == 2 ? p2 : p3;
     };
@@ -205,19 +222,22 @@ __global__ __launch_bounds__(256) void pa_beam_steal_kernel(PaSplitArgs a) {
       u32x4 k[NI], v[NI];
     };
     // shared: this wave's quarter (pieces gi QP .. gi QP + QP - 1 of
-    // [K pieces | V pieces]); private: the wave's whole page.  Piece indices
-    // stay compile-time (a branch on the wave-uniform gi per piece), so the
-    // stages never leave registers.
+    // [K pieces | V pieces]); private: the wave's whole page.  Every call
+    // issues the same 2 NI load instructions (pieces not loaded get a
+    // zero-record descriptor: no bytes move), so the compiler's wait for the
+    // current item is a counted vmcnt(2 NI) behind the next item's loads,
+    // never vmcnt(0); piece indices stay compile-time (no scratch).
     auto issue = [&](Stage& st, int pg, bool shared) {
       const auto krs = rsrc(a.k_pool, pg), vrs = rsrc(a.v_pool, pg);
+      const auto none = rsrc(a.k_pool, -1);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        if (!shared || i / QP == gi)
-          st.k[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, lane_off + i * 1024, 0, kKvLoadAux);
+        st.k[i] = __builtin_amdgcn_raw_buffer_load_b128(!shared || i / QP == gi ? krs : none,
+                                                         lane_off + i * 1024, 0, kKvLoadAux);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
-        if (!shared || (NI + i) / QP == gi)
-          st.v[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, lane_off + i * 1024, 0, kKvLoadAux);
+        st.v[i] = __builtin_amdgcn_raw_buffer_load_b128(!shared || (NI + i) / QP == gi ? vrs : none,
+                                                         lane_off + i * 1024, 0, kKvLoadAux);
     };
     int buf = 0;  // LDS buffer of the next shared item
     auto compute = [&](Stage& st, int pg, bool shared, int tile) {
@@ -239,75 +259,68 @@ __global__ __launch_bounds__(256) void pa_beam_steal_kernel(PaSplitArgs a) {
       tile_math(st.k, st.v, pg, tile);
     };
 
-    // batch 0 is static (tiles [s KB, (s + 1) KB)); wave 0 asks for the next
-    // one at once and publishes it at mid-batch
-    int t0 = s * KB;
-    int nb = 0;  // batches taken
-    int ids = load_ids(t0);
-    unsigned got = 0;
-    if (gi == 0 && lane == 0)
-      got = __hip_atomic_fetch_add(ctr, (unsigned)KB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int nt0 = -1, nids = -1;
-    int k = 0;  // item of the current batch
+    // Batch 0 is static (items [s KB, (s + 1) KB)); wave 0 asks for the next
+    // batch when a batch starts and publishes the answer at mid-batch, where
+    // the next batch's page ids start loading.  The body of one batch is
+    // unrolled over its KB items, so stage indices and every wait are
+    // compile-time (a counted vmcnt behind the next item's 2 NI loads).
     struct Item {
       bool have, shared;
       int pg, tile;
     };
-    // the item after the current one (item k of batch t0): within this batch,
-    // else the first of the next batch; at mid-batch the next batch's start
-    // reaches every wave and its page ids start loading
-    auto next_item = [&]() {
-      if (k == KB / 2) {
-        if (gi == 0 && lane == 0) next_lds[nb & 1] = (int)got;
-        __syncthreads();
-        nt0 = a.nsplit * KB + next_lds[nb & 1];
-        nids = load_ids(nt0);
-      }
-      Item it{false, false, -1, 0};
-      if (k + 1 < KB && t0 + k + 1 < ntiles) {
-        it.have = true;
-        it.tile = t0 + k + 1;
-        it.pg = item_page(ids, k + 1, it.shared);
-      } else if (k + 1 >= KB && nt0 >= 0 && nt0 < ntiles) {
-        it.have = true;
-        it.tile = nt0;
-        it.pg = item_page(nids, 0, it.shared);
-      }
-      return it;
-    };
-    auto advance = [&]() {  // the next item becomes the current one
-      if (k + 1 >= KB) {  // on to the next batch; ask for the one after it
-        t0 = nt0;
-        ids = nids;
-        nt0 = -1;
-        k = 0;
-        ++nb;
-        if (gi == 0 && lane == 0)
-          got = __hip_atomic_fetch_add(ctr, (unsigned)KB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        ++k;
-      }
-    };
-    Stage sa, sb;
-    Item cur{t0 < ntiles, false, -1, t0};
-    if (cur.have) {
-      cur.pg = item_page(ids, 0, cur.shared);
-      issue(sa, cur.pg, cur.shared);
-    }
+    Stage st[2];
+    int t0 = s * KB;
+    int ids = load_ids(t0);
+    unsigned got = 0;
+    Item cur{t0 < ntiles, false, -1, tile_of(t0)};
+    if (cur.have) cur.pg = item_page(ids, 0, cur.shared);
+    issue(st[0], cur.have ? cur.pg : -1, cur.shared);
+    int nb = 0;  // batches taken
     while (cur.have) {
-      Item nx = next_item();  // current item in sa
-      if (nx.have) issue(sb, nx.pg, nx.shared);
-      compute(sa, cur.pg, cur.shared, cur.tile);
-      if (!nx.have) break;
-      advance();
-      cur = nx;
-      nx = next_item();  // current item in sb
-      if (nx.have) issue(sa, nx.pg, nx.shared);
-      compute(sb, cur.pg, cur.shared, cur.tile);
-      if (!nx.have) break;
-      advance();
-      cur = nx;
+      int nt0 = -1, nids = -1;
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        // the request for the next batch, and its answer at mid-batch, sit in
+        // the same unrolled body: the wait for it is a counted vmcnt
+        if (k == 0 && gi == 0 && lane == 0)
+          got = __hip_atomic_fetch_add(ctr, (unsigned)KB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == KB / 2) {
+          if (gi == 0 && lane == 0) next_lds[nb & 1] = (int)got;
+          const unsigned long long tm0 = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
+          __syncthreads();
+          if constexpr (STAMPS) t_mid += __builtin_amdgcn_s_memrealtime() - tm0;
+          nt0 = a.nsplit * KB + next_lds[nb & 1];
+          nids = load_ids(nt0);
+        }
+        Item nx{false, false, -1, 0};
+        if (k + 1 < KB) {
+          if (t0 + k + 1 < ntiles) {
+            nx.have = true;
+            nx.tile = tile_of(t0 + k + 1);
+            nx.pg = item_page(ids, k + 1, nx.shared);
+          }
+        } else if (nt0 < ntiles) {
+          nx.have = true;
+          nx.tile = tile_of(nt0);
+          nx.pg = item_page(nids, 0, nx.shared);
+        }
+        issue(st[(k + 1) & 1], nx.have ? nx.pg : -1, nx.shared);
+        if (cur.have) {
+          if constexpr (STAMPS) {
+            if (n_items == 0) t_first = __builtin_amdgcn_s_memrealtime();
+            ++n_items;
+            n_shared += cur.shared ? 1 : 0;
+          }
+          compute(st[k & 1], cur.pg, cur.shared, cur.tile);
+        }
+        cur = nx;
+      }
+      // on to the next batch (its first item is in flight in st[0])
+      t0 = nt0;
+      ids = nids;
+      ++nb;
     }
+    if constexpr (STAMPS) t_last = __builtin_amdgcn_s_memrealtime();
     // every wave is past its last counter access: one arrival per workgroup,
     // the last one resets both counters for the next launch
     __syncthreads();
@@ -347,6 +360,22 @@ __global__ __launch_bounds__(256) void pa_beam_steal_kernel(PaSplitArgs a) {
     if (lane == 0) {
       a.part_ml[pidx * 2] = m;
       a.part_ml[pidx * 2 + 1] = l;
+    }
+  }
+  if constexpr (STAMPS) {
+    if (lane == 0) {
+      unsigned long long* o = a.stamps + ((size_t)blockIdx.x * 4 + gi) * 8;
+      unsigned hw = 0, xcc = 0;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      o[0] = t_entry;
+      o[1] = t_first;
+      o[2] = t_last;
+      o[3] = __builtin_amdgcn_s_memrealtime();
+      o[4] = (unsigned long long)n_items;
+      o[5] = (unsigned long long)n_shared;
+      o[6] = t_mid;
+      o[7] = ((unsigned long long)xcc << 32) | hw;
     }
   }
 }

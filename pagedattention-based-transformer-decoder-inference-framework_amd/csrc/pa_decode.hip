@@ -309,6 +309,13 @@ bool oproj_fuse_on() {
   return true;
 #endif
 }
+bool beam_steal_on() {
+#if LLM_TUNING
+  return env_int("LLM_BEAM_STEAL", 0) == 1;  // read per launch
+#else
+  return false;
+#endif
+}
 // The steal form's exchange splits a shared page's 2 NI pieces of 1 KiB over
 // the 4 waves: NI = TS D / 512 even (fp16 pages of 2, 4 or 8 KiB).
 constexpr bool steal_shape_ok(int D, int TS) {
@@ -383,13 +390,27 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
     return tune_launch_beam4(a, D, TS, st);
   }
 #endif
+#if LLM_TUNING
   if (a.group == 4 && !direct && a.steal) {  // dynamic tile assignment (pa_beam_steal.hpp)
     if constexpr (steal_shape_ok(D, TS)) {
-      hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS>), grid, block, 0, st, a);
+      if constexpr (D == 128 && TS == 16) {
+        if (env_int("LLM_BEAM_STAMPS", 0) == 1) {  // per-wave timestamps (scripts/beam_stamps.py)
+          *beam = true;
+          return tune_launch_steal_stamps(a, grid, st);
+        }
+      }
+      const int kb = env_int("LLM_STEAL_KB", kStealBatch);  // tuning: tiles per batch
+      if (env_int("LLM_STEAL_MINW", 0) == 3)  // tuning: no 128-VGPR cap (3 waves per SIMD)
+        hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, kStealBatch, 3>), grid, block, 0, st, a);
+      else if (kb == 2) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 2>), grid, block, 0, st, a);
+      else if (kb == 8) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 8>), grid, block, 0, st, a);
+      else if (kb == 16) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 16>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS>), grid, block, 0, st, a);
       *beam = true;
       return hipGetLastError();
     }
   }
+#endif
   if (a.group == 4 && !direct && ST == 2) {
     // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
     // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
@@ -799,7 +820,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     return LLM_OK;
   }
   unsigned* steal_ctr = nullptr;
-  if (steal_form)
+  if (steal_form && LLM_TUNING)
     steal_ctr = rows && rows->beam_ctr ? rows->beam_ctr
                                        : standalone_steal_counters(2 * (size_t)((B + 3) / 4) * H);
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");

@@ -63,6 +63,11 @@ int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 // merge (PaRowOutputs::o_acc); always in the product build.
 bool oproj_fuse_on();
 
+// Whether the decoder's beam launches assign tiles while they run
+// (PaRowOutputs::beam_ctr, pa_beam_steal.hpp): tuning build, LLM_BEAM_STEAL=1
+// (same-box it lost to the static BEAM form).
+bool beam_steal_on();
+
 // Split merge of per-(row, head, split) partial softmax states into rows
 // (out fp32 [B][H*D] and/or the rows->q / out16 o_proj inputs); row b's
 // context is context_lens[b], or ctx_p0 + b + 1 when context_lens is NULL and

@@ -6,6 +6,7 @@
 // register-stage / cache-policy variants (scripts/bench_kernels.py,
 // scripts/tune_attention.py).
 #include "tune/pa_decode_tune.hpp"
+#include "pa_beam_steal.hpp"
 
 namespace llm {
 
@@ -808,6 +809,29 @@ hipError_t tune_launch_beam_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t
   return hipGetLastError();
 }
 
+// The decoder's steal form (D 128, page 16) with per-wave stamps
+// (pa_beam_steal_kernel STAMPS, 8 per wave; pa_tune_stamps8 copies them).
+static unsigned long long* g_stamps8 = nullptr;
+static size_t g_stamps8_cap = 0, g_stamps8_waves = 0;
+
+hipError_t tune_launch_steal_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t st) {
+  const size_t waves = (size_t)grid.x * 4;
+  if (waves > g_stamps8_cap) {
+    if (g_stamps8) (void)hipFree(g_stamps8);
+    g_stamps8 = nullptr;
+    g_stamps8_cap = 0;
+    if (hipMalloc(&g_stamps8, waves * 8 * sizeof(unsigned long long)) != hipSuccess)
+      return hipErrorOutOfMemory;
+    g_stamps8_cap = waves;
+  }
+  (void)hipMemsetAsync(g_stamps8, 0, waves * 8 * sizeof(unsigned long long), st);
+  PaSplitArgs a = a0;
+  a.stamps = g_stamps8;
+  g_stamps8_waves = waves;
+  hipLaunchKernelGGL((pa_beam_steal_kernel<128, 16, kStealBatch, 4, true>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 hipError_t tune_beam_mfma_occupancy(int* blocks) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, pa_beam_mfma_kernel<0>, 256, 0);
 }
@@ -815,6 +839,18 @@ hipError_t tune_beam_mfma_occupancy(int* blocks) {
 }  // namespace llm
 
 using namespace llm;
+
+// Tuning hook: the last steal-form stamps (8 per wave) into host; returns the
+// waves copied (-1: none recorded).
+extern "C" long long pa_tune_stamps8(unsigned long long* host, long long max_waves) {
+  if (!g_stamps8 || !host) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  const size_t n = std::min<size_t>((size_t)max_waves, g_stamps8_waves);
+  if (hipMemcpy(host, g_stamps8, n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return -1;
+  return (long long)n;
+}
 
 // Tuning hook: the last LLM_BEAM_STAMPS launch's per-wave stamps (5 per wave,
 // pa_split_kernel STAMPS) into host (room for max_waves); returns the waves

@@ -20,6 +20,8 @@ hipError_t tune_launch_beam_loads_only(const PaSplitArgs& a, dim3 grid, hipStrea
 // chunks (pa_split_kernel RING), optionally with the trivial consumer
 // the shipped form with per-wave timestamps (STAMPS; pa_tune_stamps copies them)
 hipError_t tune_launch_beam_stamps(const PaSplitArgs& a, dim3 grid, hipStream_t st);
+// the decoder's steal form with per-wave stamps (pa_tune_stamps8 copies them)
+hipError_t tune_launch_steal_stamps(const PaSplitArgs& a, dim3 grid, hipStream_t st);
 hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st, int ring,
                                  bool load_only);
 

@@ -65,6 +65,9 @@ def main():
         dec.run_attention(0, st)
     torch.cuda.synchronize()
     os.environ.pop("LLM_BEAM_STAMPS")
+    if form & 64:  # the steal form: 8 stamps per wave
+        steal_report(lib, args)
+        return
     buf = np.zeros((1 << 16, 5), np.uint64)
     n = lib.pa_tune_stamps(buf.ctypes.data, buf.shape[0])
     if n <= 0:
@@ -94,6 +97,40 @@ def main():
     print("exit p90 per XCC:", [round(float(np.percentile(ex[xcc == x], 90)), 2)
                                 for x in range(8) if np.any(xcc == x)])
     np.save(os.path.join(ROOT, "gpurun_out", f"beam_stamps_{args.config}.npy"), s)
+
+
+def steal_report(lib, args):
+    """pa_beam_steal_kernel STAMPS: entry, first tile, after the last tile,
+    exit, tiles, shared tiles, mid-batch barrier ticks, HW_ID per wave."""
+    lib.pa_tune_stamps8.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    lib.pa_tune_stamps8.restype = ctypes.c_longlong
+    buf = np.zeros((1 << 16, 8), np.uint64)
+    n = lib.pa_tune_stamps8(buf.ctypes.data, buf.shape[0])
+    if n <= 0:
+        raise SystemExit("no steal stamps recorded")
+    s = buf[:n].astype(np.int64)
+    live = s[:, 3] > 0
+    s = s[live]
+    t0 = s[:, 0].min()
+    ent, fst, lst, ex = [(s[:, i] - t0) / 100.0 for i in range(4)]
+    items, shared, mid = s[:, 4], s[:, 5], s[:, 6] / 100.0
+    xcc = (s[:, 7] >> 32) & 0xF
+    print(f"steal form: waves {len(s)} of {n}; kernel span {ex.max():.2f} us")
+    print("entry      ", pct(ent))
+    print("first tile ", pct(fst))
+    print("start-up   ", pct(fst - ent))
+    print("tiles span ", pct(lst - fst))
+    print("exit       ", pct(ex))
+    print("tiles/wave ", pct(items))
+    print("shared/wave", pct(shared))
+    print("mid-barrier", pct(mid))
+    print("us per tile", pct((lst - fst) / np.maximum(items, 1)))
+    grid = np.arange(0, ex.max() + 1, 1.0)
+    active = [(np.sum((fst <= t) & (lst > t))) for t in grid]
+    print("waves on tiles per us:", " ".join(str(a) for a in active))
+    print("exit p90 per XCC:", [round(float(np.percentile(ex[xcc == x], 90)), 2)
+                                for x in range(8) if np.any(xcc == x)])
+    np.save(os.path.join(ROOT, "gpurun_out", f"steal_stamps_{args.config}.npy"), s)
 
 
 if __name__ == "__main__":

@@ -204,16 +204,15 @@ def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
 def test_int8_c4_beam_state_attention_vs_oracle(gpu, oracle):
     """The C4 bench state (begin_beams(8, 4, 3840, 256): 240 shared tiles per
     sequence through page-table forks, 16 private per beam) at C3 head dims,
-    2 layers: the beam-group launch with tiles assigned while it runs
-    (pa_beam_steal.hpp), merged and quantised by pa_merge_row_kernel, against
-    the oracle on every row."""
+    2 layers: the beam-group launch with cost-balanced splits, merged and
+    quantised by pa_merge_row_kernel, against the oracle on every row."""
     from oracle.oracle import OracleDecoder
     rows, T = 32, 4096
     w, dec = _int8_decoder(oracle, 2, 16, 128, 512, T + 8, rows, seed=52)
     taps = _Taps(dec, w["cfg"], rows)
     dec.begin_beams(8, 4, 3840, 256, 99, True)
     ns, form = dec.attention_plan()
-    assert form == (FORM_SPLIT_MERGE_ROW | FORM_BEAM | FORM_STEAL) and ns >= 8, (ns, form)
+    assert form == (FORM_SPLIT_MERGE_ROW | FORM_BEAM) and ns >= 8, (ns, form)
     odec = OracleDecoder(oracle, w, rows)
     distinct = decoder_kv_to_oracle(dec, odec, rows, T)
     # shared prefixes are read from shared pages: 8 x 16 x 240 + 32 x 16 x 16
