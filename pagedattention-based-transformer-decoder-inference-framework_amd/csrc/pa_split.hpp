@@ -197,23 +197,39 @@ void pa_split_kernel(PaSplitArgs a) {
   // BEAM: the shared path runs only when all 4 rows exist, route to a valid
   // page-table row and hold the same context (a uniform decision: every wave
   // of the workgroup evaluates the same 4 rows, before any early return).
+  // The 4 rows' beam ids and contexts are loaded side by side (no early exit:
+  // a row-by-row loop made them 4 dependent round trips), and this wave's own
+  // row's first kPfx page-table ids (the prefix scan below) are requested as
+  // soon as its beam id is known, before the contexts decide whether the
+  // group shares: under the other workgroups' KV streams each dependent round
+  // trip here cost about a microsecond of start-up.
+  constexpr int kPfx = 512;
   bool share = false;
   int grow[4] = {0, 0, 0, 0};  // BEAM: the group's page-table rows
+  int idv[BEAM ? kPfx / 64 : 1];
+  const bool pfx_on = BEAM && a.balance16 >= 16 && a.pps == 0 && a.nsplit > 1;
   if constexpr (BEAM) {
-    share = true;
     const int g0 = b - gi;
-    int T0 = -1;
+    int Ti[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int bi = g0 + i;
-      if (bi >= a.B) { share = false; break; }
-      const int ri = a.beam_ids ? a.beam_ids[bi] : bi;
-      int Ti = a.context_lens ? a.context_lens[bi] : a.T;
-      Ti = min(max(Ti, 0), a.T);
-      if (ri < 0 || ri >= a.num_beams || (i > 0 && Ti != T0)) { share = false; break; }
-      T0 = Ti;
-      grow[i] = ri;
+      const int bi = min(g0 + i, a.B - 1);
+      grow[i] = a.beam_ids ? a.beam_ids[bi] : bi;
+      Ti[i] = a.context_lens ? a.context_lens[bi] : a.T;
     }
+    const bool own_ok = grow[gi] >= 0 && grow[gi] < a.num_beams;
+    const int32_t* prow = a.page_table + ((size_t)(own_ok ? grow[gi] : 0) * a.H + h) * a.max_tiles;
+    const int lim0 = min(a.max_tiles, kPfx);
+#pragma unroll
+    for (int k = 0; k < kPfx / 64; ++k) {
+      const int t = 64 * k + lane;
+      idv[k] = pfx_on && own_ok && t < lim0 ? prow[t] : -1;
+    }
+    share = g0 + 3 < a.B;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      share = share && grow[i] >= 0 && grow[i] < a.num_beams &&
+              min(max(Ti[i], 0), a.T) == min(max(Ti[0], 0), a.T);
   }
   if (b >= a.B) return;
   const int bh = b * a.H + h;
@@ -230,7 +246,6 @@ void pa_split_kernel(PaSplitArgs a) {
   }
   // BEAM: the page ids of the group's 4 rows, tiles [0, pfx_lim), read once
   // by the prefix scan below and reused for this split's page ids
-  constexpr int kPfx = 512;
   __shared__ int pfx_lds[BEAM ? 4 : 1][BEAM ? kPfx : 1];
   int pfx_lim = 0;
   if constexpr (BEAM) {
@@ -245,18 +260,14 @@ void pa_split_kernel(PaSplitArgs a) {
     // in ONE round trip (8 loads per lane in flight, then one barrier): the
     // 64-tile rounds this replaced cost a dependent page-table load and two
     // barriers each before the first KV load could issue.
-    if (share && a.balance16 >= 16 && a.pps == 0 && a.nsplit > 1 && ntiles > 0) {
+    if (share && pfx_on && ntiles > 0) {
       const int32_t* prow = a.page_table + ((size_t)grow[gi] * a.H + h) * a.max_tiles;
       const int lim = min(ntiles, kPfx);
-      int idv[kPfx / 64];
 #pragma unroll
       for (int k = 0; k < kPfx / 64; ++k) {
         const int t = 64 * k + lane;
-        idv[k] = t < lim ? prow[t] : -1;
+        pfx_lds[gi][t] = t >= lim || idv[k] >= a.num_pages ? -1 : idv[k];
       }
-#pragma unroll
-      for (int k = 0; k < kPfx / 64; ++k)
-        pfx_lds[gi][64 * k + lane] = idv[k] >= a.num_pages ? -1 : idv[k];
       __syncthreads();
       int nsh_t = 0;
       for (int blk = 0; blk < lim; blk += 64) {
