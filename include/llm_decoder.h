@@ -95,8 +95,9 @@ int pa_decode_pages_per_split(int B, int H, int T, int page_size, int max_tiles)
 #define LLM_PA_FORM_WG_MERGE 3        /* splits merged inside the split workgroup */
 #define LLM_PA_FORM_BEAM 16
 #define LLM_PA_FORM_OPROJ 32 /* FP16 decoder: o_proj fused into the workgroup merge */
-#define LLM_PA_FORM_STEAL 64 /* beam groups: tiles assigned to the splits while the launch
-                                runs (decoder launches; with LLM_PA_FORM_BEAM) */
+#define LLM_PA_FORM_STEAL 64 /* tuning library only (LLM_BEAM_STEAL=1): beam groups with
+                                tiles assigned to the splits while the launch runs (with
+                                LLM_PA_FORM_BEAM); the product never reports it */
 int pa_decode_plan(const pa_kv_view* kv, int B, int H, int D, int T, int pages_per_split,
                    int row_group, int* nsplit, int* form);
 
