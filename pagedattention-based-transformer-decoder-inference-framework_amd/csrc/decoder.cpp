@@ -533,7 +533,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
   } else {
     ro.out16 = R.act;
   }
-  if (R.row_group >= 4) ro.beam_ctr = beam_ctr.p;
+  if (R.row_group >= 4 && beam_steal_on()) ro.beam_ctr = beam_ctr.p;
   return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
                             R.row_group, plan);

@@ -318,27 +318,17 @@ bool beam_steal_on() {
 }
 // The steal form's exchange splits a shared page's 2 NI pieces of 1 KiB over
 // the 4 waves: NI = TS D / 512 even (fp16 pages of 2, 4 or 8 KiB).
-constexpr int kBeamPoolDiv = 8;
 constexpr bool steal_shape_ok(int D, int TS) {
   return D >= 8 && D <= 512 && (TS * D) % 1024 == 0 && TS * D * 2 <= 8192;
 }
-// The static beam form's shared-tile pool: the last 1/8 of each group's
-// shared prefix (tuning: LLM_BEAM_POOL_DIV, 0 = off).
-int beam_pool_div() {
-#if LLM_TUNING
-  return env_int("LLM_BEAM_POOL_DIV", kBeamPoolDiv);  // read per launch
-#else
-  return kBeamPoolDiv;
-#endif
-}
 // Standalone beam launches (pa_decode C entry, no decoder-owned counters):
-// the tuning build's LLM_BEAM_STEAL=1 / LLM_BEAM_POOL=1 give them counters of
-// its own (one buffer per process: launches must not overlap).
+// the tuning build's LLM_BEAM_STEAL=1 runs the steal form on counters of its
+// own (one buffer per process: launches must not overlap).
 unsigned* standalone_steal_counters(size_t n) {
 #if LLM_TUNING
   static unsigned* buf = nullptr;
   static size_t cap = 0;
-  if (env_int("LLM_BEAM_STEAL", 0) != 1 && env_int("LLM_BEAM_POOL", 0) != 1) return nullptr;
+  if (env_int("LLM_BEAM_STEAL", 0) != 1) return nullptr;
   if (n > cap) {
     if (buf) (void)hipFree(buf);
     buf = nullptr;
@@ -401,7 +391,7 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
   }
 #endif
 #if LLM_TUNING
-  if (a.group == 4 && !direct && a.steal && a.steal_dyn) {  // dynamic tile assignment (pa_beam_steal.hpp)
+  if (a.group == 4 && !direct && a.steal) {  // dynamic tile assignment (pa_beam_steal.hpp)
     if constexpr (steal_shape_ok(D, TS)) {
       if constexpr (D == 128 && TS == 16) {
         if (env_int("LLM_BEAM_STAMPS", 0) == 1) {  // per-wave timestamps (scripts/beam_stamps.py)
@@ -812,11 +802,10 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                 "pa_decode: at most 128 splits of at most 128 pages per row (raise "
                 "pages_per_split, or pass 0; T <= 16384 pages)");
   const bool direct = nsplit <= 1;
-  // beam groups of 4 fp16 rows with counters: the static form's shared-tile
-  // pool, or (tuning, LLM_BEAM_STEAL=1) fully dynamic tile assignment
-  const bool beam_launch = row_group >= 4 && !direct && kv->kv_dtype == LLM_F16 &&
-                           pps_fixed <= 0 && !use_beam4 && !beam_mfma_on();
-  const bool steal_form = beam_launch && steal_shape_ok(D, TS) && beam_steal_on();
+  // beam groups of 4 fp16 rows with counters: dynamic tile assignment
+  const bool steal_form = row_group >= 4 && !direct && kv->kv_dtype == LLM_F16 &&
+                          pps_fixed <= 0 && !use_beam4 && !beam_mfma_on() &&
+                          steal_shape_ok(D, TS);
   if (plan) {
     const int group = std::max(1, std::min(row_group, 4));
     const bool wg = wgm_ok && !direct && group == 1 && nsplit <= kWgmMaxSplits;
@@ -831,7 +820,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     return LLM_OK;
   }
   unsigned* steal_ctr = nullptr;
-  if (beam_launch)
+  if (steal_form && LLM_TUNING)
     steal_ctr = rows && rows->beam_ctr ? rows->beam_ctr
                                        : standalone_steal_counters(2 * (size_t)((B + 3) / 4) * H);
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
@@ -869,8 +858,6 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   a.balance16 = beam_balance16();
   a.beam4 = use_beam4 ? 1 : 0;
   a.steal = a.group == 4 ? steal_ctr : nullptr;
-  a.steal_dyn = a.steal && steal_form ? 1 : 0;
-  a.pool_div = a.steal && !steal_form ? beam_pool_div() : 0;
   if (wgm) {
     a.wgm = 1;
     a.out16 = static_cast<_Float16*>(rows->out16);

@@ -38,10 +38,8 @@ struct PaRowOutputs {
   int* o_flag = nullptr;
   // Beam-group launches (row_group 4, fp16 KV): 2 * ceil(B / 4) * H counters,
   // zero before the first launch and left at zero by every launch; with them
-  // the BEAM form leaves the last 1/8 of each group's shared prefix out of its
-  // static split boundaries and the workgroups that finish first draw those
-  // tiles from a pool (the tuning build's LLM_BEAM_STEAL=1 instead assigns
-  // every tile while the launch runs, pa_beam_steal.hpp, LLM_PA_FORM_STEAL)
+  // the launch assigns tiles dynamically (pa_beam_steal.hpp,
+  // LLM_PA_FORM_STEAL), without them it runs the static BEAM form
   unsigned* beam_ctr = nullptr;
 };
 

@@ -92,11 +92,6 @@ struct PaSplitArgs {
   // per (sequence group, head) the next-batch counter and the arrival count,
   // zero at launch, left at zero by the launch
   unsigned* steal;
-  // BEAM with counters (steal set, pool_div > 0): the last nsh / pool_div
-  // tiles of each group's shared prefix are left out of the static split
-  // boundaries and drawn one at a time by the workgroups that finish first
-  int pool_div;
-  int steal_dyn;  // tuning: with steal, run pa_beam_steal_kernel instead (LLM_BEAM_STEAL=1)
   // tuning (pa_split_kernel STAMPS): per wave wid, s_memrealtime (100 MHz) at
   // entry, at the first KV load, after the shared-prefix chunks, at exit, and
   // the wave's HW_ID (CU / SIMD / XCC placement): stamps[wid * 5 + 0..4]
@@ -253,7 +248,6 @@ void pa_split_kernel(PaSplitArgs a) {
   // by the prefix scan below and reused for this split's page ids
   __shared__ int pfx_lds[BEAM ? 4 : 1][BEAM ? kPfx : 1];
   int pfx_lim = 0;
-  int pool_P = 0, nshS = 0;  // BEAM pool: tiles [nshS, nshS + pool_P) of the shared prefix
   if constexpr (BEAM) {
     // Cost-balanced splits: a split's beam-private tiles are loaded by every
     // wave (4x the per-wave bytes of a shared tile, which the workgroup loads
@@ -308,35 +302,27 @@ void pa_split_kernel(PaSplitArgs a) {
       }
       nsh_t = min(nsh_t, ntiles);
       if (nsh_t > 0 && nsh_t < ntiles) {
-        // the pool (U == 1 pages per chunk, shared tiles held in pfx_lds)
-        const int pp = U == 1 && a.steal && a.pool_div > 0 && nsh_t <= pfx_lim ? nsh_t / a.pool_div : 0;
-        const int sh = nsh_t - pp;  // shared tiles under static boundaries
-        const int nt = ntiles - pp;  // static tiles: t' < sh shared, t' >= sh private (t = t' + pp)
         const long long A = 16, P = a.balance16, ns = a.nsplit;
-        const long long C = A * sh + P * (nt - sh);
-        auto start = [&](int k) -> int {  // first (static) tile of split k
+        const long long C = A * nsh_t + P * (ntiles - nsh_t);
+        auto start = [&](int k) -> int {  // first tile of split k
           if (k <= 0) return 0;
-          if (k >= ns) return nt;
+          if (k >= ns) return ntiles;
           const long long x = (C * k + ns - 1) / ns;
-          if (x <= A * sh) return (int)((x + A - 1) / A);
-          return (int)min<long long>(nt, sh + (x - A * sh + P - 1) / P);
+          if (x <= A * nsh_t) return (int)((x + A - 1) / A);
+          return (int)min<long long>(ntiles, nsh_t + (x - A * nsh_t + P - 1) / P);
         };
         // every tile costs >= A, so no split holds more than C/ns/A + 2 tiles
         if ((C + ns - 1) / ns / A + 2 <= kMaxPps) {
           tile0 = start(s);
           count = start(s + 1) - tile0;
-          pool_P = pp;
-          nshS = sh;
         }
       }
     }
   }
   const int c = lane % LPT;
   const int g = lane / LPT;
-  // tile of the split's j-th static item (past the pool when it is on)
-  auto tile_at = [&](int j) { return tile0 + j < nshS || pool_P == 0 ? tile0 + j : tile0 + j + pool_P; };
 
-  if (count <= 0 && pool_P == 0) {
+  if (count <= 0) {
     if constexpr (BEAM && !DIRECT) {
       // the merge of a beam launch reads every split: an empty one holds
       // (m, l, acc) = (sentinel, 0, 0)
@@ -364,14 +350,13 @@ void pa_split_kernel(PaSplitArgs a) {
   // Page ids of this split: lane j holds pages j and 64 + j
   // (PageTable::lookup semantics: out of range or >= num_pages -> missing).
   int pid0 = -1, pid1 = -1;
-  count = max(count, 0);  // (a pool workgroup with no static tiles)
-  if (BEAM && count > 0 && tile_at(count - 1) < pfx_lim) {  // (r is row gi: read by the prefix scan)
-    if (lane < count) pid0 = pfx_lds[gi][tile_at(lane)];
-    if (64 + lane < count) pid1 = pfx_lds[gi][tile_at(64 + lane)];
+  if (BEAM && tile0 + count <= pfx_lim) {  // (r is the group's row gi: read by the prefix scan)
+    if (lane < count) pid0 = pfx_lds[gi][tile0 + lane];
+    if (64 + lane < count) pid1 = pfx_lds[gi][tile0 + 64 + lane];
   } else if (r >= 0 && r < a.num_beams) {
-    const int32_t* row = a.page_table + ((size_t)r * a.H + h) * a.max_tiles;
-    if (lane < count) pid0 = row[tile_at(lane)];
-    if (64 + lane < count) pid1 = row[tile_at(64 + lane)];
+    const int32_t* row = a.page_table + ((size_t)r * a.H + h) * a.max_tiles + tile0;
+    if (lane < count) pid0 = row[lane];
+    if (64 + lane < count) pid1 = row[64 + lane];
     if (pid0 >= a.num_pages) pid0 = -1;
     if (pid1 >= a.num_pages) pid1 = -1;
   }
@@ -418,10 +403,7 @@ void pa_split_kernel(PaSplitArgs a) {
     }
   };
 
-  // pool_pg >= -1: one pool tile (page pool_pg, tile pool_tile) instead of
-  // the split's items p0 ..
-  auto compute = [&](const u32x4 (&kk)[NR], const u32x4 (&vv)[NR], int p0, int pool_pg = -2,
-                     int pool_tile = 0) {
+  auto compute = [&](const u32x4 (&kk)[NR], const u32x4 (&vv)[NR], int p0) {
     if constexpr (LOAD_ONLY) {  // tuning: the same stream with a trivial consumer
       uint32_t x = 0;
 #pragma unroll
@@ -467,12 +449,10 @@ void pa_split_kernel(PaSplitArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = p0 + u;
-      const bool pool = pool_pg >= -1;
-      const int pg = pool ? pool_pg : page_of(min(j, kMaxPps - 1));
-      const bool ok = (pool || j < count) && (pg >= 0);
-      const int tile = pool ? pool_tile : tile_at(j);
-      const int tok_base = tile * TS + g;
-      if (FULLPATH && ok && (tile + 1) * TS <= Tb)
+      const int pg = page_of(min(j, kMaxPps - 1));
+      const bool ok = (j < count) && (pg >= 0);
+      const int tok_base = (tile0 + j) * TS + g;
+      if (FULLPATH && ok && (tile0 + j + 1) * TS <= Tb)
         page_math(std::true_type{}, u, ok, tok_base);
       else
         page_math(std::false_type{}, u, ok, tok_base);
@@ -634,63 +614,6 @@ void pa_split_kernel(PaSplitArgs a) {
       if (ch + 1 >= nchunks) break;
       issue(kA, vA, (ch + 2) * U);
       compute(kB, vB, (ch + 1) * U);
-    }
-  }
-  if constexpr (BEAM && !DIRECT && U == 1) {
-    // The pool: the workgroups that finish their static tiles first draw the
-    // remaining shared tiles one at a time (a per-(group, head) counter; the
-    // request for the next tile is in flight while the current one is
-    // computed).  Every workgroup of a pooled group then adds one arrival to
-    // the group's second counter after its counter accesses have retired, and
-    // the last arrival zeroes both for the next launch.
-    if (pool_P > 0) {
-      constexpr int QP = NR / 2;
-      __shared__ __attribute__((aligned(16))) u32x4 pool_buf[2 * NR][64];
-      __shared__ int pool_lds[2];
-      unsigned* ctr = a.steal + 2 * gh;
-      unsigned got = 0;
-      if (gi == 0 && lane == 0)
-        got = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int it = 0;; ++it) {
-        if (gi == 0 && lane == 0) pool_lds[it & 1] = (int)got;
-        __syncthreads();  // (also: every wave is done reading pool_buf)
-        const int idx = pool_lds[it & 1];
-        if (idx >= pool_P) break;
-        if (gi == 0 && lane == 0)
-          got = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int tile = nshS + idx;
-        const int pg = pfx_lds[0][tile];  // shared: the same page in all 4 rows
-        const bool ok = pg >= 0;
-        const size_t off = (size_t)(ok ? pg : 0) * a.page_stride;
-        u32x4 qr[QP];
-#pragma unroll
-        for (int t = 0; t < QP; ++t) {
-          const int q = gi * QP + t;
-          const uint8_t* pool = q < NR ? a.k_pool : a.v_pool;
-          const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(pool + off), (short)0,
-                                                            ok ? PAGE_BYTES : 0, 0x00020000);
-          qr[t] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + (q % NR) * 1024, 0, AUX);
-        }
-#pragma unroll
-        for (int t = 0; t < QP; ++t) pool_buf[gi * QP + t][lane] = qr[t];
-        __syncthreads();
-        u32x4 kk[NR], vv[NR];
-#pragma unroll
-        for (int p = 0; p < NR; ++p) {
-          kk[p] = pool_buf[p][lane];
-          vv[p] = pool_buf[NR + p][lane];
-        }
-        compute(kk, vv, 0, pg, tile);
-      }
-      if (gi == 0 && lane == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unused last request retired
-        const unsigned old =
-            __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == (unsigned)a.nsplit - 1u) {
-          __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
     }
   }
 

@@ -97,9 +97,8 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
     cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1),
     its one-wave-per-group kernel (LLM_BEAM4=1), the shipped form fed by an
-    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits), the decoder's
-    shared-tile pool (LLM_BEAM_POOL=1) and the dynamic-assignment form
-    (LLM_BEAM_STEAL=1)."""
+    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits) and the
+    dynamic-assignment form (LLM_BEAM_STEAL=1)."""
     import torch
     import llm_capi
     rng = np.random.default_rng(B * 7 + T)
@@ -189,21 +188,6 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     # counters, LLM_BEAM_STEAL=1).  Run three times: the counters must come
     # back to zero after every launch (a stale counter skips tiles).  Which
     # split sums which tile varies run to run, so only fp32 merge rounding differs.
-    # ... the decoder's form: the static boundaries over all but the last
-    # 1/8 (and, stressed, 1/2) of each group's shared prefix, those tiles drawn
-    # from a pool by the workgroups that finish first (LLM_BEAM_POOL=1 gives the
-    # standalone launch the tuning build's own counters)
-    monkeypatch.setenv("LLM_BEAM_POOL", "1")
-    for div in ("8", "2", "8"):
-        monkeypatch.setenv("LLM_BEAM_POOL_DIV", div)
-        outp = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
-                                  beam_ids=d(beam_ids), row_group=4,
-                                  lib=llm_capi.load_tune()).cpu().numpy()
-        assert np.isfinite(outp).all()
-        assert_parity(outp, ref, 1e-3)
-        assert rel_err(outp, plain) < 1e-5, (div, rel_err(outp, plain))
-    monkeypatch.delenv("LLM_BEAM_POOL")
-    monkeypatch.delenv("LLM_BEAM_POOL_DIV")
     monkeypatch.setenv("LLM_BEAM_STEAL", "1")
     for _ in range(3):
         outs = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
