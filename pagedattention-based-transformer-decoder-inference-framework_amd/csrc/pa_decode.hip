@@ -113,20 +113,30 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
     const size_t bh = (size_t)b * a.H + h;
     const float* ml = a.part_ml + bh * a.nsplit * 2;
     const float* pa = a.part_acc + bh * a.nsplit * a.D;
-    // split weights, lane-parallel: lane holds splits lane and 64 + lane
-    const float m0 = lane < ns ? ml[2 * lane] : kNegSentinel;
-    const float m1 = 64 + lane < ns ? ml[2 * (64 + lane)] : kNegSentinel;
-    const float l0 = lane < ns ? ml[2 * lane + 1] : 0.f;
-    const float l1 = 64 + lane < ns ? ml[2 * (64 + lane) + 1] : 0.f;
+    // split weights, lane-parallel: lane holds splits lane and 64 + lane.
+    // Every load's address depends on kernel arguments only (clamped to the
+    // launch's nsplit), so they issue together with the context_lens load
+    // instead of after it (one round trip, not two); the row's split count
+    // ns masks the values afterwards (splits past ns may hold stale bits).
+    const int nsl = max(a.nsplit - 1, 0);
+    const float m0r = ml[2 * min(lane, nsl)], l0r = ml[2 * min(lane, nsl) + 1];
+    const float m1r = ml[2 * min(64 + lane, nsl)], l1r = ml[2 * min(64 + lane, nsl) + 1];
     float v[kMergeBatch][DPL];
 #pragma unroll
     for (int s2 = 0; s2 < kMergeBatch; ++s2)
 #pragma unroll
       for (int j = 0; j < DPL; ++j) {
         const int d = lane + 64 * j;
-        // unconditional loads (clamped in range) so all issue before the first wait
-        v[s2][j] = pa[(size_t)min(s2, max(ns - 1, 0)) * a.D + min(d, a.D - 1)];
+        v[s2][j] = pa[(size_t)min(s2, nsl) * a.D + min(d, a.D - 1)];
       }
+    const float m0 = lane < ns ? m0r : kNegSentinel;
+    const float m1 = 64 + lane < ns ? m1r : kNegSentinel;
+    const float l0 = lane < ns ? l0r : 0.f;
+    const float l1 = 64 + lane < ns ? l1r : 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < kMergeBatch; ++s2)
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) v[s2][j] = s2 < ns ? v[s2][j] : 0.f;
     const float M = ln_wave_max(fmaxf(m0, m1));
     float* dst = row + h * a.D;
     if (ns <= 0 || M <= 0.5f * kNegSentinel) {
