@@ -72,17 +72,17 @@ def _tokens(mode, world, rank, global_rows):
     return np.random.default_rng(1234).integers(0, V, global_rows).astype(np.int32)[lo:hi]
 
 
-def _run(rows, world, rank, shard_rows, gather, first, row0=None):
+def _run(rows, world, rank, shard_rows, gather, first, row0=None, staging="host"):
     import torch
     import dist_decode
     dec = _decoder(rows, row0)
     with torch.cuda.stream(torch.cuda.Stream()):  # bench.py's explicit stream
         sd = dist_decode.ShardedDecode(dist_decode.HipDecoderStep(dec), rows, V, world=world,
                                        rank=rank, shard_rows=shard_rows, gather=gather,
-                                       staging="host", keep=True)
+                                       staging=staging, keep=True)
         elapsed = dist_decode.timed_run(sd, WARMUP, STEPS, [int(t) for t in first],
                                         timer_device="cpu")
-        return [t.numpy().copy() for t in sd.finish()], elapsed
+        return [t.cpu().numpy().copy() for t in sd.finish()], elapsed
 
 
 def test_hip_step_refuses_the_default_stream(gpu):
@@ -94,7 +94,7 @@ def test_hip_step_refuses_the_default_stream(gpu):
         dist_decode.HipDecoderStep(_decoder(1))
 
 
-def _worker(rank, world, port, mode, gather, global_rows, q, long_ctx=False):
+def _worker(rank, world, port, mode, gather, global_rows, q, long_ctx=False, staging="host"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     for p in (str(ROOT), str(PKG)):
         sys.path.insert(0, p)
@@ -113,7 +113,7 @@ def _worker(rank, world, port, mode, gather, global_rows, q, long_ctx=False):
     if long_ctx:
         row0 = rank * ROWS_PER_RANK if mode == "weak" else dist_decode.shard_range(global_rows, world, rank)[0]
     collected, elapsed = _run(rows, world, rank, shard_rows, gather,
-                              _tokens(mode, world, rank, global_rows), row0)
+                              _tokens(mode, world, rank, global_rows), row0, staging)
     if rank == 0:
         q.put((collected, elapsed))
     dist.barrier()
@@ -195,3 +195,79 @@ def test_sharded_hip_decode_long_context(gpu, mode, global_rows):
         for r in np.nonzero(ga != gb)[0]:
             assert b[r, gb[r]] - b[r, ga[r]] <= 1e-3 * np.abs(b[r]).max(), (s_, r)
     print(f"sharded vs one process at {PROMPT}+ tokens: worst logits rel err {worst:.2e}")
+
+
+@pytest.mark.parametrize("gather", ["logits", "ids"])
+def test_sharded_hip_decode_device_staging(gpu, gather):
+    """The staging="device" branch bench.py runs over RCCL: each step's rows
+    are written straight into the RowGatherer's device buffers and the gather
+    takes the device tensors (gloo's gather accepts them and moves them
+    through host memory itself; on the 8-GPU node the same tensors go to
+    RCCL).  Weak sharding: the equal-shard torch.distributed gather.  Rank 0's
+    gathered steps must equal one process stepping all rows, bit for bit."""
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "weak", gather, 0, q, False, "device"))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        collected, _ = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    first = np.concatenate([_tokens("weak", world, r, 0) for r in range(world)])
+    ref, _ = _run(len(first), 1, 0, None, gather, first)
+    assert len(collected) == WARMUP + STEPS
+    for s in range(WARMUP + STEPS):
+        a, b = collected[s], ref[s]
+        assert a.shape == b.shape, (s, a.shape, b.shape)
+        assert np.array_equal(a.view(np.uint32) if gather == "logits" else a,
+                              b.view(np.uint32) if gather == "logits" else b), s
+
+
+def _rccl_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (str(ROOT), str(PKG)):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+    import dist_decode
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    with torch.cuda.stream(torch.cuda.Stream()):
+        t = torch.arange(3 * V, dtype=torch.float32, device="cuda").view(3, V)
+        recv = [torch.full((3, V), -1.0, device="cuda")]
+        dist_decode._gather(t, recv, 0, True).wait()
+        ids = torch.arange(7, dtype=torch.int32, device="cuda")
+        rids = [torch.zeros(7, dtype=torch.int32, device="cuda")]
+        dist_decode._gather(ids, rids, 0, True).wait()
+        torch.cuda.synchronize()
+        q.put((torch.equal(recv[0], t), torch.equal(rids[0], ids), dist.get_backend()))
+    dist.destroy_process_group()
+
+
+def test_rccl_gather_of_device_rows(gpu):
+    """The RCCL leg of the device-staged gather on the one-GPU box: a one-rank
+    nccl (= RCCL) group gathers device logits and id rows with the same
+    dist_decode._gather call the multi-GPU loop makes (RCCL refuses two ranks
+    on one device, so this is as far as one GPU takes it)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        ok_logits, ok_ids, backend = q.get(timeout=100)
+    finally:
+        p.join(timeout=30)
+        if p.exitcode is None:
+            p.kill()
+    assert p.exitcode == 0, p.exitcode
+    assert backend == "nccl" and ok_logits and ok_ids
