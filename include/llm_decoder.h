@@ -182,8 +182,12 @@ typedef struct pa_decode_options {
 /* pa_decode with the options above.  With every option off (top_k 0, top_p 1,
  * eos -1, no outputs) this is pa_decode with sm_scale = 1/temperature^2 (the
  * hot path; workspace as for pa_decode).  Otherwise one workgroup per (b, h)
- * keeps the row's scores in LDS: T <= 8192 and D <= 256 (else
- * LLM_ERR_UNSUPPORTED); workspace is unused. */
+ * keeps the row's scores in LDS when T <= 8192 (workspace unused), and in the
+ * workspace for longer rows: T > 8192 needs an 8-byte aligned workspace of
+ * pa_decode_ex_workspace_bytes(B, H, T) bytes (else LLM_ERR_INVALID); like
+ * cpu_paged_attention_forward (attention_cpu/cpu_attention_kernel.cpp:61) the
+ * context has no upper bound.  D <= 256 (else LLM_ERR_UNSUPPORTED). */
+size_t pa_decode_ex_workspace_bytes(int B, int H, int T);
 int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
                  const int32_t* context_lens, int B, int H, int D, int T,
                  const pa_decode_options* opt, void* workspace, size_t workspace_bytes,

@@ -563,4 +563,6 @@ PYBIND11_MODULE(llm_decoder, m) {
         py::arg("bias") = 0, py::arg("activation") = "", py::arg("stream") = 0);
   m.def("workspace_bytes", &pa_decode_workspace_bytes, py::arg("B"), py::arg("H"), py::arg("D"),
         py::arg("max_tiles"), py::arg("pages_per_split") = 0);
+  m.def("filter_workspace_bytes", &pa_decode_ex_workspace_bytes, py::arg("B"), py::arg("H"),
+        py::arg("T"));
 }

@@ -12,7 +12,10 @@
 // kernel runs when a caller asks for them.
 //
 // One workgroup per (row b, head h).  The whole row of scores lives in LDS
-// (T <= 8192): scores -> softmax -> (sort by (prob, index) descending ->
+// (T <= 8192), or, for longer rows, in the caller's workspace (the row's
+// scores and sort keys, pa_decode_ex_workspace_bytes; only its own workgroup
+// touches them, so the barriers that order the LDS form order these too):
+// scores -> softmax -> (sort by (prob, index) descending ->
 // top-k / top-p mask) -> EOS threshold -> AV.  The sort key is
 // (prob bits << 32 | index): probabilities are >= 0, so the unsigned order of
 // the key is exactly std::greater on pair<float, int> — the order
@@ -44,6 +47,9 @@ struct PaFilterArgs {
   int num_pages, num_beams, max_tiles;
   size_t page_stride;  // elements from page p to page p + 1
   float temperature;
+  uint64_t* ws_key;   // [B*H][Tp] sort keys (the workspace form)
+  float* ws_sc;       // [B*H][Tp] scores / probabilities (the workspace form)
+  int Tp;             // row stride of ws_key / ws_sc
   int top_k;
   float top_p;
   int eos;
@@ -76,14 +82,16 @@ __device__ float block_reduce(float x, float* sh) {
   return r;
 }
 
-template <int KVT>
+template <int KVT, bool WS>
 __global__ __launch_bounds__(kFilterThreads) void pa_filter_kernel(PaFilterArgs a) {
   __shared__ float qs[256];
-  __shared__ float sc[kFilterMaxT];  // scores, then probabilities
-  __shared__ uint64_t key[kFilterMaxT];
+  __shared__ float lsc[WS ? 1 : kFilterMaxT];  // scores, then probabilities
+  __shared__ uint64_t lkey[WS ? kFilterThreads / 2 : kFilterMaxT];  // WS: the AV reduction only
   __shared__ float sh[kFilterThreads / 64];
   const int tid = threadIdx.x;
   const int bh = blockIdx.x;
+  float* sc = WS ? a.ws_sc + (size_t)bh * a.Tp : lsc;
+  uint64_t* key = WS ? a.ws_key + (size_t)bh * a.Tp : lkey;
   const int b = bh / a.H, h = bh % a.H;
   const int D = a.D;
   const int r = a.beam_ids ? a.beam_ids[b] : b;
@@ -212,7 +220,7 @@ __global__ __launch_bounds__(kFilterThreads) void pa_filter_kernel(PaFilterArgs 
       if (pg < 0) continue;
       acc += p * kv_elem<KVT>(a.v_pool, (size_t)pg * a.page_stride + (size_t)(t % a.TS) * D + d);
     }
-  float* red = reinterpret_cast<float*>(key);
+  float* red = reinterpret_cast<float*>(lkey);
   __syncthreads();
   if (g < G) red[g * D + d] = acc;
   __syncthreads();
@@ -226,6 +234,19 @@ __global__ __launch_bounds__(kFilterThreads) void pa_filter_kernel(PaFilterArgs 
 }  // namespace llm
 
 using namespace llm;
+
+namespace {
+int filter_row_stride(int T) {  // the bitonic sort's power-of-two length
+  int Tp = 1;
+  while (Tp < T) Tp <<= 1;
+  return Tp;
+}
+}  // namespace
+
+extern "C" size_t pa_decode_ex_workspace_bytes(int B, int H, int T) {
+  if (B <= 0 || H <= 0 || T <= kFilterMaxT) return 0;
+  return (size_t)B * H * filter_row_stride(T) * (sizeof(uint64_t) + sizeof(float));
+}
 
 extern "C" int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out,
                             const int32_t* beam_ids, const int32_t* context_lens, int B, int H,
@@ -253,9 +274,13 @@ extern "C" int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out,
                                           kv_elem_size(kv->kv_dtype) &&
                    kv->page_stride % 16 == 0),
               "pa_decode_ex: page_stride must be 0 or >= one page and a multiple of 16");
-  if (T > kFilterMaxT || D > 256)
-    return fail(LLM_ERR_UNSUPPORTED, "pa_decode_ex: filters / weight outputs need T <= 8192 and "
-                                     "D <= 256");
+  if (D > 256) return fail(LLM_ERR_UNSUPPORTED, "pa_decode_ex: filters / weight outputs need D <= 256");
+  const bool ws_form = T > kFilterMaxT;
+  const size_t need = pa_decode_ex_workspace_bytes(B, H, T);
+  LLM_REQUIRE(!ws_form || (workspace != nullptr && workspace_bytes >= need &&
+                           reinterpret_cast<uintptr_t>(workspace) % 8 == 0),
+              "pa_decode_ex: T > 8192 with filters needs an 8-byte aligned workspace of "
+              "pa_decode_ex_workspace_bytes(B, H, T)");
   PaFilterArgs a{};
   a.k_pool = static_cast<const uint8_t*>(kv->k_pool);
   a.v_pool = static_cast<const uint8_t*>(kv->v_pool);
@@ -270,19 +295,32 @@ extern "C" int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out,
   a.num_pages = kv->num_pages; a.num_beams = kv->num_beams; a.max_tiles = kv->max_tiles;
   a.page_stride = kv_view_page_stride(*kv) / std::max(1, kv_elem_size(kv->kv_dtype));
   a.temperature = opt->temperature;
+  if (ws_form) {
+    a.Tp = filter_row_stride(T);
+    a.ws_key = static_cast<uint64_t*>(workspace);
+    a.ws_sc = reinterpret_cast<float*>(a.ws_key + (size_t)B * H * a.Tp);
+  }
   a.top_k = opt->top_k;
   a.top_p = opt->top_p;
   a.eos = opt->eos_token;
   a.eos_thr = opt->eos_threshold;
   hipStream_t st = as_stream(stream);
   const dim3 grid(B * H), block(kFilterThreads);
+#define LLM_FILTER_LAUNCH(KVT)                                                  \
+  do {                                                                          \
+    if (ws_form)                                                                \
+      hipLaunchKernelGGL((pa_filter_kernel<KVT, true>), grid, block, 0, st, a);  \
+    else                                                                        \
+      hipLaunchKernelGGL((pa_filter_kernel<KVT, false>), grid, block, 0, st, a); \
+  } while (0)
   switch (kv->kv_dtype) {
-    case LLM_F16: hipLaunchKernelGGL(pa_filter_kernel<LLM_F16>, grid, block, 0, st, a); break;
-    case LLM_BF16: hipLaunchKernelGGL(pa_filter_kernel<LLM_BF16>, grid, block, 0, st, a); break;
-    case LLM_F32: hipLaunchKernelGGL(pa_filter_kernel<LLM_F32>, grid, block, 0, st, a); break;
-    case LLM_I8: hipLaunchKernelGGL(pa_filter_kernel<LLM_I8>, grid, block, 0, st, a); break;
+    case LLM_F16: LLM_FILTER_LAUNCH(LLM_F16); break;
+    case LLM_BF16: LLM_FILTER_LAUNCH(LLM_BF16); break;
+    case LLM_F32: LLM_FILTER_LAUNCH(LLM_F32); break;
+    case LLM_I8: LLM_FILTER_LAUNCH(LLM_I8); break;
     default: return fail(LLM_ERR_INVALID, "pa_decode_ex: kv_dtype");
   }
+#undef LLM_FILTER_LAUNCH
   LLM_HIP_RET(hipGetLastError());
   return LLM_OK;
 }

@@ -68,6 +68,7 @@ _SIGS = {
                              c_int, c_int, c_int, c_int, ctypes.POINTER(PaDecodeOptions),
                              c_void_p, c_size_t, c_void_p]),
     "pa_prefill_workspace_bytes": (c_size_t, [ctypes.POINTER(PaKvView), c_int, c_int]),
+    "pa_decode_ex_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "pa_prefill": (c_int, [ctypes.POINTER(PaKvView), c_void_p, c_int, c_void_p, c_int, c_int,
                            c_int, c_int, c_float, c_void_p, c_size_t, c_void_p]),
     "gemm_packed_bytes": (c_size_t, [c_int, c_int, c_int]),
@@ -266,8 +267,9 @@ def pa_decode_ex(q, k_pool, v_pool, page_table, *, T, beam_ids=None, context_len
                           eos_threshold=eos_threshold,
                           probs_out=None if probs is None else probs.data_ptr(),
                           scores_out=None if scores is None else scores.data_ptr())
-    ws_bytes = lib.pa_decode_workspace_bytes(B, H, D, page_table.shape[2], 0)
-    ws = torch.empty(max(ws_bytes, 4), dtype=torch.uint8, device=q.device)
+    ws_bytes = max(lib.pa_decode_workspace_bytes(B, H, D, page_table.shape[2], 0),
+                   lib.pa_decode_ex_workspace_bytes(B, H, T))
+    ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=q.device)
     check(lib.pa_decode_ex(ctypes.byref(view), ptr(q), ptr(out), ptr(beam_ids), ptr(context_lens),
                            B, H, D, T, ctypes.byref(opt), ptr(ws), ws_bytes, stream_ptr(stream)))
     return (out, probs, scores) if want_probs else out

@@ -80,7 +80,7 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.pa_decode(ctypes.byref(fake), *args) == llm_capi.LLM_ERR_INVALID
     assert b"kv_dtype" in lib.llm_last_error()
     # pa_decode_ex: temperature must be positive; the filtered kernel keeps a
-    # row of scores in LDS (T <= 8192)
+    # row of scores in LDS (T <= 8192), in the workspace beyond
     fake.kv_dtype = llm_capi.LLM_F16
     fake.head_dim = 64
     opt = llm_capi.PaDecodeOptions(temperature=0.0, top_k=0, top_p=1.0, eos_token=-1)
@@ -89,7 +89,12 @@ def test_invalid_arguments_rejected_before_any_launch():
     opt.temperature, opt.top_k = 1.0, 5
     big = exargs[:7] + (8193,)
     assert lib.pa_decode_ex(ctypes.byref(fake), *big, ctypes.byref(opt), None, 0,
-                            None) == llm_capi.LLM_ERR_UNSUPPORTED
+                            None) == llm_capi.LLM_ERR_INVALID
+    assert b"pa_decode_ex_workspace_bytes" in lib.llm_last_error()
+    assert lib.pa_decode_ex_workspace_bytes(1, 1, 8192) == 0
+    assert lib.pa_decode_ex_workspace_bytes(1, 1, 8193) == 16384 * 12
+    assert lib.pa_decode_ex_workspace_bytes(3, 2, 20000) == 3 * 2 * 32768 * 12
+    assert lib.pa_decode_ex_workspace_bytes(0, 2, 20000) == 0
     # pa_prefill: NULL view / q / out, unsupported pools (int8) and positions
     # past the page table are rejected on the host
     assert lib.pa_prefill(None, None, 0, None, 0, 0, 0, 1, 1.0, None, 0, None) == 1

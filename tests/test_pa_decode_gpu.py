@@ -376,6 +376,67 @@ def test_pa_decode_ex_random_vs_oracle(gpu, oracle, kv_dtype, top_k, top_p, eos)
         assert_parity(hot, out, RTOL)
 
 
+@pytest.mark.parametrize("kv_dtype", ["float16", "int8"])
+@pytest.mark.parametrize("top_k,top_p,eos", [(0, 1.0, -1), (64, 1.0, -1), (0, 0.5, -1),
+                                             (300, 0.9, -1), (0, 1.0, 12000)])
+def test_pa_decode_ex_long_rows_vs_oracle(gpu, oracle, kv_dtype, top_k, top_p, eos):
+    """Rows past the LDS form's 8192 tokens: the filtered kernel keeps each
+    row's scores and sort keys in the workspace (pa_decode_ex_workspace_bytes),
+    as cpu_paged_attention_forward has no context bound
+    (attention_cpu/cpu_attention_kernel.cpp:61).  Ragged rows up to 20000
+    tokens, beam routing, a missing page, against the oracle."""
+    import torch
+    import llm_capi
+    dt = getattr(torch, kv_dtype)
+    rng = np.random.default_rng(top_k + 7 * eos + 11)
+    B, H, D, T, ts, beams = 3, 2, 64, 20000, 16, 2
+    nt = (T + ts - 1) // ts
+    num_pages = beams * H * nt + 2
+    q = (rng.standard_normal((B, H, D)) * (0.1 if dt == torch.int8 else 0.5)).astype(np.float32)
+    kd, kf = _kv_elems(rng, dt, (num_pages, ts, D), 0.5)
+    vd, vf = _kv_elems(rng, dt, (num_pages, ts, D), 1.0)
+    pt = rng.permutation(num_pages)[: beams * H * nt].astype(np.int32).reshape(beams, H, nt)
+    pt[0, 1, 600] = -1
+    beam_ids = np.array([1, 0, 1], np.int32)
+    lens = np.array([20000, 8193, 13001], np.int32)
+    ref, rp, rs = oracle.paged_attention(q, kf, vf, pt, T=T, beam_ids=beam_ids, context_lens=lens,
+                                         temperature=0.9, top_k=top_k, top_p=top_p,
+                                         eos_token=eos, eos_threshold=0.0, want_probs=True)
+    out, probs, scores = llm_capi.pa_decode_ex(
+        _dev(q), kd, vd, _dev(pt), T=T, beam_ids=_dev(beam_ids), context_lens=_dev(lens),
+        temperature=0.9, top_k=top_k, top_p=top_p, eos_token=eos, eos_threshold=0.0,
+        want_probs=True)
+    out, probs, scores = (x.cpu().numpy() for x in (out, probs, scores))
+    assert_parity(out, ref, RTOL)
+    assert_parity(probs, rp, RTOL)
+    np.testing.assert_array_equal(probs > 0, rp > 0)
+    _check_scores(scores, rs)
+
+
+def test_pa_decode_ex_workspace_form_equals_lds_form(gpu):
+    """The same rows (<= 8192 tokens) through the LDS form (T 8192) and the
+    workspace form (T 8193, the rows' context_lens unchanged): the same
+    arithmetic in the same order, so out and probs are bit-identical."""
+    import torch
+    import llm_capi
+    rng = np.random.default_rng(5)
+    B, H, D, ts = 2, 3, 128, 16
+    nt = 8208 // ts
+    num_pages = H * nt + 1
+    q = (rng.standard_normal((B, H, D)) * 0.3).astype(np.float32)
+    kd, _ = _kv_elems(rng, torch.float16, (num_pages, ts, D), 0.5)
+    vd, _ = _kv_elems(rng, torch.float16, (num_pages, ts, D), 1.0)
+    pt = rng.permutation(num_pages)[: H * nt].astype(np.int32).reshape(1, H, nt)
+    lens = _dev(np.array([8192, 5000], np.int32))
+    res = []
+    for T in (8192, 8193):
+        out, probs, _ = llm_capi.pa_decode_ex(_dev(q), kd, vd, _dev(pt), T=T, context_lens=lens,
+                                              top_k=100, top_p=0.8, want_probs=True)
+        res.append((out.cpu().numpy(), probs[:, :, :8192].cpu().numpy()))
+    assert np.array_equal(res[0][0].view(np.uint32), res[1][0].view(np.uint32))
+    assert np.array_equal(res[0][1].view(np.uint32), res[1][1].view(np.uint32))
+
+
 def test_paged_attention_binding_filters(gpu, oracle):
     """llm_decoder.paged_attention (AttentionCUDA::forward surface) with top_k /
     top_p now runs the filtered kernel instead of refusing."""
