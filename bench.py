@@ -1,21 +1,27 @@
 #!/usr/bin/env python3
 """Decode throughput of the MI355X paged-attention INT8 decoder (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5|c1]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 Workload (default, BASELINE config C3): INT8Decoder with 24 layers, 16 heads,
-head_dim 128 (hidden 2048, inter 8192, vocab 50257), 64 sequences per GPU,
+head_dim 128 (hidden 2048, inter 8192, vocab 50257), a batch of 64 sequences,
 every sequence holding a KV context of 8192 tokens in shuffled 16-token pages
 (synthetic random fp16 K/V, random-init int8 weights — no checkpoints exist).
-A step = one full decode step of all 64 rows (embed, 24 x {LN, qkv GEMM, KV
+A step = one full decode step of all rows (embed, 24 x {LN, qkv GEMM, KV
 append, paged attention, o GEMM, LN, fc1, fc2}, tied LM head, argmax), replayed
 as a hipGraph; generation continues from step to step (the context grows).
 
-Multi-GPU: one process per GPU, sequences sharded by rank (weak scaling: 64 per
-GPU), no exchange inside a step; the final logits of every step are gathered to
-rank 0 over RCCL (the one collective of the design).  value = tokens/s of the
-whole job = 64 * N / t_step, t_step = max over ranks.
+Multi-GPU: one process per GPU.  `--gpus N` with no WORLD_SIZE in the
+environment starts the N ranks itself (before torch or any GPU is touched);
+under torch.distributed.run it checks that the launcher started exactly N.
+Sequences are sharded by rank, no exchange inside a step; the final logits of
+every step are gathered to rank 0 over RCCL (the one collective of the design).
+The headline follows the metric's own mode: C3 / C2 scale STRONG,
+the config's batch (64 for C3) split over the N ranks; C5 (64 rows per GPU by
+definition) and C4 scale weak.  At N > 1 a strong line also carries the weak
+figure (the config's batch on EVERY rank) as `weak_scaling`.  value = tokens/s
+of the whole job = rows of all ranks / t_step, t_step = max over ranks.
 
 Also reported (one JSON line on rank 0):
   roofline     the paged-attention launch (the dominant kernel), timed live with
@@ -43,9 +49,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 CONFIGS = {
     # BASELINE.json configs[2]: the metric's config
-    "c3": dict(cls="INT8Decoder", L=24, H=16, D=128, V=50257, B=64, T=8192, ts=16,
+    "c3": dict(cls="INT8Decoder", L=24, H=16, D=128, V=50257, B=64, T=8192, ts=16, strong=True,
                workload="C3: INT8 decoder (MFMA i8 matmuls + fp16 paged attention), "
-                        "24-layer/16-head/d=128, 64 seqs/GPU, KV context 8192, page 16"),
+                        "24-layer/16-head/d=128, batch 64, KV context 8192, page 16"),
     # BASELINE.json configs[3]: beam=4 decode over forked prefixes (C3 model dims,
     # SURVEY §8 C4 build decision): 8 sequences x 4 beams; each sequence's first
     # 3840 tokens live in shared (forked) pages, each beam holds 256 private tokens
@@ -65,8 +71,8 @@ CONFIGS = {
                workload="C1: INT8 decoder, 2-layer/4-head/d=64, batch 1, KV context 128, "
                         "page 16"),
     # BASELINE.json configs[1]
-    "c2": dict(cls="CUDADecoder", L=12, H=12, D=64, V=50257, B=16, T=2048, ts=16,
-               workload="C2: fp16 paged decode, 12-layer/12-head/d=64, 16 seqs/GPU, "
+    "c2": dict(cls="CUDADecoder", L=12, H=12, D=64, V=50257, B=16, T=2048, ts=16, strong=True,
+               workload="C2: fp16 paged decode, 12-layer/12-head/d=64, batch 16, "
                         "KV context 2048, page 16"),
 }
 
@@ -319,6 +325,142 @@ def load_traffic(cfg_name):
         return None
 
 
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` with no WORLD_SIZE in the environment: start N copies
+    of this script as ranks 0..N-1 (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT in their environment, the
+    same variables torch.distributed.run sets).  This process has not imported
+    torch and never touches a GPU: it only waits.  When a rank fails, the
+    others are terminated (a rank blocked in a collective would wait for its
+    dead peer forever) and the launcher exits non-zero.  Rank 0 prints the one
+    JSON line; the other ranks print nothing on stdout."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    script = str(Path(__file__).resolve())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rc, deadline = 0, None
+    live = dict(enumerate(procs))
+    while live:
+        for r, p in list(live.items()):
+            c = p.poll()
+            if c is None:
+                continue
+            del live[r]
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                log(f"bench.py launcher: rank {r} exited with {c}; stopping ranks {sorted(live)}")
+                for q in live.values():
+                    q.terminate()
+                deadline = time.time() + 30
+        if deadline is not None and time.time() > deadline:
+            for q in live.values():
+                q.kill()
+            deadline = None
+        time.sleep(0.1)
+    return rc
+
+
+class StubStep:
+    """`--stub-step` (CPU tests of the launcher and of the multi-rank line
+    only): a deterministic host step in place of the HIP decoder.  logits[b, v]
+    and the next ids are cheap integer functions of the row's token."""
+
+    def __init__(self, rows, vocab):
+        self.rows, self.V = rows, vocab
+        self.next = np.zeros(rows, np.int64)
+
+    def __call__(self, tokens, logits_out):
+        import torch
+        tok = np.asarray(tokens if tokens is not None else self.next, np.int64)
+        if logits_out is not None:
+            v = torch.arange(self.V, dtype=torch.int64)
+            t = torch.from_numpy(tok)[:, None]
+            logits_out.copy_(((t * 31 + v * 7) % 97).to(torch.float32))
+        self.next = (tok * 31 + 7) % self.V
+
+    def ids_into(self, out):
+        import torch
+        out.copy_(torch.from_numpy(self.next.astype(np.int32)))
+
+
+def run_mode(cfg, args, world, rank, strong, backend, stub):
+    """Build this rank's decoder for one scaling mode and time the sharded
+    decode loop (dist_decode.ShardedDecode + timed_run).  strong: the global
+    batch (args.global_batch or the config's batch) split over the ranks,
+    first tokens one global draw, sharded; weak: the config's batch on every
+    rank, first tokens drawn per rank.  Returns (stats, decoder or None)."""
+    import dist_decode
+    B, T = cfg["B"], cfg["T"]
+    shard_rows, G = None, B * world
+    if strong:
+        G = args.global_batch or B
+        if G < world:
+            raise SystemExit(f"bench.py: a global batch of {G} rows needs >= {world} rows")
+        shard_rows = dist_decode.shard_sizes(G, world)
+        B = shard_rows[rank]
+        lo, hi = dist_decode.shard_range(G, world, rank)
+        tokens = np.random.default_rng(args.seed).integers(0, cfg["V"], G).astype(np.int32)[lo:hi]
+    else:
+        tokens = np.random.default_rng(args.seed + rank).integers(0, cfg["V"], B).astype(np.int32)
+    host_gather = world > 1 and backend != "nccl" and not stub
+    gather = args.gather if world > 1 else "none"
+    t0 = time.time()
+    dec = None
+    if stub:
+        step = StubStep(B, cfg["V"])
+        device, sync, timer, step_times = "cpu", (lambda: None), "cpu", None
+    else:
+        import torch
+        import llm_decoder  # noqa: F401  (fails loudly if the HIP build is missing)
+        max_seq = T + 2 * (args.warmup + args.steps) + 16
+        cls = getattr(llm_decoder, cfg["cls"])
+        dec = cls(cfg["L"], cfg["H"], cfg["D"], cfg["H"] * cfg["D"], cfg["V"], max_seq,
+                  max_batch=B, page_size=cfg["ts"])
+        w = make_weights(cfg, args.seed)
+        dec.set_weights(w)
+        del w
+        if "beams" in cfg:
+            dec.begin_beams(cfg["seqs"], cfg["beams"], cfg["shared"], T - cfg["shared"],
+                            args.seed + rank, not args.contiguous_pages)
+        else:
+            dec.begin_synthetic(B, T, args.seed + rank, not args.contiguous_pages)
+        step = dist_decode.HipDecoderStep(dec)
+        device, sync = "cuda", torch.cuda.synchronize
+        timer = "cpu" if host_gather else "cuda"
+        step_times = None if host_gather else []
+    log(f"[rank {rank}] {'strong' if strong else 'weak'}: {B} rows, setup {time.time() - t0:.1f}s")
+    # each step's logits (or greedy ids, --gather ids) go to rank 0, double-buffered
+    # behind the next step; gloo rehearsals on GPUs stage them through host memory
+    sd = dist_decode.ShardedDecode(step, B, cfg["V"], world=world, rank=rank,
+                                   shard_rows=shard_rows, gather=gather, device=device,
+                                   staging="host" if host_gather else "device")
+    rank_times = []
+    elapsed = dist_decode.timed_run(sd, args.warmup, args.steps, list(map(int, tokens)),
+                                    sync=sync, timer_device=timer, step_times=step_times,
+                                    rank_times=rank_times)
+    t_step = elapsed / args.steps
+    st = {"rows_this_rank": B, "global_rows": G, "t_step": t_step,
+          "per_rank_ms_per_step": [round(t / args.steps * 1e3, 4) for t in rank_times],
+          "step_times": step_times, "value": G / t_step}
+    t_g = dist_decode.time_gather(sd, sync=sync, timer_device=timer) if world > 1 else None
+    if t_g is not None:
+        per_peer = sd.g.bufs[0].numel() * sd.g.bufs[0].element_size()
+        st["gather"] = {"what": gather, "bytes_per_rank": per_peer,
+                        "alone_ms": round(t_g * 1e3, 4),
+                        "share_of_step": round(t_g / t_step, 4),
+                        "note": "one step's gather timed on its own (max over ranks); in the "
+                                "step it is double-buffered behind the next step's compute"}
+    return st, dec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,128 +470,152 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
+                    help="auto: the metric's mode (C3 / C2 strong, C4 / C5 weak)")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: this many rows in total, sharded over the ranks "
-                         "(default: the config's batch on every rank, weak scaling)")
+                         "(default: the config's batch)")
+    ap.add_argument("--no-weak-extra", action="store_true",
+                    help="N > 1, strong headline: skip the extra weak-scaling run")
     ap.add_argument("--gather", default="logits", choices=["logits", "ids"],
                     help="N > 1: what each step gathers to rank 0 (SURVEY §8e)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--contiguous-pages", action="store_true",
                     help="sensitivity runs only: pages in allocation order instead of the "
                          "shuffled pool SURVEY §8d measures on")
+    ap.add_argument("--stub-step", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stub-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_child:  # cpu_baseline()'s child: no torch, no GPU
         print(json.dumps(cpu_baseline_run(CONFIGS[args.config], args.cpu_budget)), flush=True)
         return
-
-    import torch
-    import torch.distributed as dist
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    # stdout carries the one JSON line alone: whatever native code prints there
+    # (gloo's connection notes, RCCL / HIP chatter) goes to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if rank == args.stub_fail_rank:
+        raise SystemExit(3)
+    cfg = CONFIGS[args.config]
+    stub = args.stub_step
     # LLM_DIST_BACKEND=gloo: rehearsal of the N-rank path on fewer GPUs (ranks
     # share devices round-robin, logits gathered through host memory); the
     # real multi-GPU run is one rank per GPU over RCCL ("nccl").
-    backend = os.environ.get("LLM_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    # every step, staging copy, gather and timing event runs on ONE explicit
-    # stream (torch's default stream has handle 0, which the C ABI reads as the
-    # decoder's own non-blocking stream)
-    torch.cuda.set_stream(torch.cuda.Stream())
+    backend = "gloo" if stub else os.environ.get("LLM_DIST_BACKEND", "nccl")
+
+    import torch
+    import torch.distributed as dist
+    if not stub:
+        ndev = torch.cuda.device_count()  # (does not initialise the GPU on this image)
+        if ndev < 1:
+            raise SystemExit("bench.py: no GPU visible")
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        if backend == "nccl" and world > 1 and (ndev < lws or local >= ndev):
+            raise SystemExit(f"bench.py: --gpus {world} over RCCL needs one GPU per rank, "
+                             f"{ndev} visible to local rank {local} of {lws} (RCCL refuses two "
+                             f"ranks on one device; LLM_DIST_BACKEND=gloo rehearses N ranks "
+                             f"on fewer GPUs)")
+        local = local % ndev
+        torch.cuda.set_device(local)
+        # every step, staging copy, gather and timing event runs on ONE explicit
+        # stream (torch's default stream has handle 0, which the C ABI reads as the
+        # decoder's own non-blocking stream)
+        torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    import llm_decoder  # noqa: F401  (fails loudly if the HIP build is missing)
-    import dist_decode
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group of {dist.get_world_size()} ranks, "
+                             f"--gpus {args.gpus}")
+    pg_size = dist.get_world_size() if world > 1 else 1
 
-    cfg = CONFIGS[args.config]
-    B, T = cfg["B"], cfg["T"]
-    strong = args.global_batch > 0 and "beams" not in cfg
-    shard_rows = None
-    if strong:  # rows of this rank (ragged shards gather point to point)
-        if args.global_batch < world:
-            raise SystemExit(f"--global-batch {args.global_batch} needs >= {world} rows")
-        shard_rows = dist_decode.shard_sizes(args.global_batch, world)
-        B = shard_rows[rank]
-    hid = cfg["H"] * cfg["D"]
-    max_seq = T + args.warmup + args.steps + 8
-    cls = getattr(llm_decoder, cfg["cls"])
-    t0 = time.time()
-    dec = cls(cfg["L"], cfg["H"], cfg["D"], hid, cfg["V"], max_seq, max_batch=B,
-              page_size=cfg["ts"])
-    w = make_weights(cfg, args.seed)
-    dec.set_weights(w)
-    del w
-    if "beams" in cfg:
-        dec.begin_beams(cfg["seqs"], cfg["beams"], cfg["shared"], T - cfg["shared"],
-                        args.seed + rank, not args.contiguous_pages)
-    else:
-        dec.begin_synthetic(B, T, args.seed + rank, not args.contiguous_pages)
-    log(f"[rank {rank}] setup {time.time() - t0:.1f}s")
-
-    # the multi-rank decode loop (dist_decode.ShardedDecode / timed_run): each
-    # step's logits (or greedy ids, --gather ids) go to rank 0, double-buffered
-    # behind the next step; gloo rehearsals stage them through host memory
-    host_gather = world > 1 and backend != "nccl"
-    sd = dist_decode.ShardedDecode(
-        dist_decode.HipDecoderStep(dec), B, cfg["V"], world=world, rank=rank,
-        shard_rows=shard_rows, gather=args.gather if world > 1 else "none",
-        staging="host" if host_gather else "device")
-    tokens = np.random.default_rng(args.seed + rank).integers(0, cfg["V"], B).astype(np.int32)
-    step_times = None if host_gather else []
-    elapsed = dist_decode.timed_run(sd, args.warmup, args.steps, list(map(int, tokens)),
-                                    timer_device="cpu" if host_gather else "cuda",
-                                    step_times=step_times)
-    t_step = elapsed / args.steps
+    mode = args.scaling
+    if mode == "auto":
+        mode = "strong" if (cfg.get("strong") or args.global_batch) else "weak"
+    strong = mode == "strong" and "beams" not in cfg
+    st, dec = run_mode(cfg, args, world, rank, strong, backend, stub)
+    B, T, t_step = st["rows_this_rank"], cfg["T"], st["t_step"]
     T_mean = T + args.warmup + args.steps / 2.0
-    value = (args.global_batch if strong else B * world) / t_step
+    host_gather = world > 1 and backend != "nccl"
 
     # roofline of the dominant kernel (paged attention): the step's own launch,
-    # timed live
-    T_now = dec.context_len(0)
-    nsplit, form = dec.attention_plan()
-    t_attn = time_attention(dec)
-    attn_b = attention_launch_bytes(cfg, T_now, B, unique=True) + fused_weight_bytes(cfg, form)
-    achieved = attn_b / t_attn / 1e9
-    ratio = load_traffic(args.config)
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            # PMC-measured HBM bytes per launch (ratio from profiles/pmc_attention_<cfg>.json
-            # applied to this launch's algorithmic bytes)
-            "traffic": int(ratio * attn_b) if ratio else None,
-            "traffic_over_algorithmic": ratio,
-            "traffic_source": (f"profiles/pmc_attention_{args.config}.json: rocprofv3 PMC "
-                               "(2*FETCH_SIZE + WRITE_SIZE) / algorithmic bytes, committed, "
-                               "times this launch's algorithmic bytes (not measured in this run)")
-            if ratio else None,
-            "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}>"
-                      + (" beam-group" if form & 16 else "") + ": " + FORM_NAMES[form & 15]
-                      + (OPROJ_OUT if form & 32 else FORM_OUT.get(cfg["cls"], {}).get(form & 15, ""))
-                      + f", {nsplit} splits (the step's own launch, llm_decoder_run_attention)",
-            "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
-    if "beams" in cfg:  # logical bytes: every beam reads its whole context
-        logical = attention_launch_bytes(cfg, T_now, B)
-        roof["bytes_note"] = "achieved counts shared prefix pages once per sequence"
-        roof["logical_bytes_per_launch"] = logical
-        roof["logical_GBps"] = round(logical / t_attn / 1e9, 1)
-        t_plain = time_attention_plain(dec, cfg, B, T_now, max_seq)
-        roof["ungrouped_launch_us"] = round(t_plain * 1e6, 2)  # plain schedule, fp32 out
-    step_b = step_bytes(cfg, T_mean, B)
+    # timed live on rank 0's decoder
+    roof, step_b = None, step_bytes(cfg, T_mean, B)
+    if dec is not None and rank == 0:
+        T_now = dec.context_len(0)
+        nsplit, form = dec.attention_plan()
+        t_attn = time_attention(dec)
+        attn_b = attention_launch_bytes(cfg, T_now, B, unique=True) + fused_weight_bytes(cfg, form)
+        achieved = attn_b / t_attn / 1e9
+        ratio = load_traffic(args.config)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                # PMC-measured HBM bytes per launch (ratio from profiles/pmc_attention_<cfg>.json
+                # applied to this launch's algorithmic bytes)
+                "traffic": int(ratio * attn_b) if ratio else None,
+                "traffic_over_algorithmic": ratio,
+                "traffic_source": (f"profiles/pmc_attention_{args.config}.json: rocprofv3 PMC "
+                                   "(2*FETCH_SIZE + WRITE_SIZE) / algorithmic bytes, committed, "
+                                   "times this launch's algorithmic bytes (not measured in this "
+                                   "run)") if ratio else None,
+                "kernel": f"pa_split_kernel<D={cfg['D']},TS={cfg['ts']}>"
+                          + (" beam-group" if form & 16 else "") + ": " + FORM_NAMES[form & 15]
+                          + (OPROJ_OUT if form & 32 else FORM_OUT.get(cfg["cls"], {}).get(form & 15, ""))
+                          + f", {nsplit} splits, {B} rows (the step's own launch, "
+                            "llm_decoder_run_attention)",
+                "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
+        if "beams" in cfg:  # logical bytes: every beam reads its whole context
+            logical = attention_launch_bytes(cfg, T_now, B)
+            roof["bytes_note"] = "achieved counts shared prefix pages once per sequence"
+            roof["logical_bytes_per_launch"] = logical
+            roof["logical_GBps"] = round(logical / t_attn / 1e9, 1)
+            max_seq = T + 2 * (args.warmup + args.steps) + 16
+            t_plain = time_attention_plain(dec, cfg, B, T_now, max_seq)
+            roof["ungrouped_launch_us"] = round(t_plain * 1e6, 2)  # plain schedule, fp32 out
+
+    weak = None
+    if world > 1 and strong and not args.no_weak_extra:
+        del dec  # the strong run's pools go before the weak run allocates its own
+        import gc
+        gc.collect()
+        sw, dec = run_mode(cfg, args, world, rank, False, backend, stub)
+        weak = {"value": round(sw["value"], 2), "unit": "tokens/s",
+                "ms_per_step": round(sw["t_step"] * 1e3, 4), "batch_per_gpu": cfg["B"],
+                "global_batch": sw["global_rows"],
+                "per_rank_ms_per_step": sw["per_rank_ms_per_step"],
+                "hbm_roofline_frac_step": round(step_bytes(cfg, T_mean, cfg["B"])
+                                                / sw["t_step"] / 1e9 / HBM_PEAK_GBPS, 4),
+                "gather": sw.get("gather"),
+                "note": "the config's batch on every rank (weak scaling), same loop, run after "
+                        "the headline in the same job"}
+    del dec
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(args.config, args.cpu_budget)
         except Exception as ex:  # the baseline never blocks the GPU number
             log(f"cpu baseline failed: {ex!r}")
     if rank == 0:
+        G = st["global_rows"]
+        step_times = st["step_times"]
+        import dist_decode
+        rows_all = dist_decode.shard_sizes(G, world) if strong else [B] * world
         res = {
             "metric": "decode tokens/sec at batch=64 seq_len=8192; % HBM-roofline (1/2/4/8 GPU)"
             if args.config == "c3" else f"decode tokens/sec ({args.config})",
-            "value": round(value, 2),
+            "value": round(st["value"], 2),
             "unit": "tokens/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -457,26 +623,35 @@ def main():
             "ms_per_step": round(t_step * 1e3, 4),
             "ms_per_step_median_hip_events": round(float(np.median(step_times)) * 1e3, 4)
             if step_times else None,
+            "per_rank_ms_per_step": st["per_rank_ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "int8 GEMM (i32 acc) + fp16 KV attention (fp32 acc)"
             if cfg["cls"] == "INT8Decoder" else "fp16 GEMM + fp16 KV attention (fp32 acc)",
             "data": "synthetic (random-init weights, random fp16 KV context, "
-                    + ("pages in allocation order)" if args.contiguous_pages else "shuffled pages)"),
-            "config": {"workload": cfg["workload"] + (f"; strong scaling: {args.global_batch} rows "
-                                                      f"over {world} GPU(s)" if strong else ""),
-                       "global_batch": args.global_batch if strong else B * world,
-                       "batch_per_gpu": B, "seq_len": T, "page_size": cfg["ts"],
+                    + ("pages in allocation order)" if args.contiguous_pages else "shuffled pages)")
+                    + ("; STUB host step (launcher test, no decoder)" if stub else ""),
+            "config": {"workload": cfg["workload"] + (f"; strong scaling: {G} rows over {world} "
+                                                      f"GPU(s)" if strong else
+                                                      f"; weak scaling: {B} rows per GPU"),
+                       "global_batch": G, "batch_per_gpu": B, "seq_len": T,
+                       "page_size": cfg["ts"],
                        "parallelism": "single GPU (no collective)" if world == 1
                        else f"batch-sharded x{world} (RCCL {args.gather} gather to rank 0)"
                        if not host_gather else f"batch-sharded x{world} ({backend} rehearsal)"},
-            "hbm_roofline_frac_step": round(step_b / t_step / 1e9 / HBM_PEAK_GBPS, 4),
+            "rccl_ranks": pg_size if backend == "nccl" and world > 1 else 0,
+            "process_group": {"backend": backend if world > 1 else None, "size": pg_size},
+            "gather": st.get("gather"),
+            # mean over the GPUs of each one's algorithmic step bytes / t_step / 8 TB/s
+            "hbm_roofline_frac_step": round(sum(step_bytes(cfg, T_mean, r) for r in rows_all)
+                                            / world / t_step / 1e9 / HBM_PEAK_GBPS, 4),
             "step_bytes": int(step_b),
             "roofline": roof,
+            "weak_scaling": weak,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res), file=json_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

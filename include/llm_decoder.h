@@ -30,8 +30,8 @@ enum llm_status {
   LLM_ERR_OOM = 4,          /* device or page-pool allocation failure */
   LLM_ERR_IO = 5,           /* weight / cache file I/O */
   LLM_ERR_RANGE = 6         /* a device value left a fixed-point accumulator's range (the
-                               FP16 decoder's fused o_proj); reported by llm_decoder_sync /
-                               a synchronous step, cleared by the next begin / generate */
+                               FP16 decoder's fused o_proj); reported ONCE per clamp, by the
+                               first llm_decoder_sync or synchronous step after it */
 };
 
 /* Element types.  KV pools may be any of the four (the T of
@@ -186,7 +186,8 @@ typedef struct pa_decode_options {
  * workspace for longer rows: T > 8192 needs an 8-byte aligned workspace of
  * pa_decode_ex_workspace_bytes(B, H, T) bytes (else LLM_ERR_INVALID); like
  * cpu_paged_attention_forward (attention_cpu/cpu_attention_kernel.cpp:61) the
- * context has no upper bound.  D <= 256 (else LLM_ERR_UNSUPPORTED). */
+ * context has no practical upper bound: D <= 256 and T <= 2^30 (else
+ * LLM_ERR_UNSUPPORTED; the workspace size is then 0). */
 size_t pa_decode_ex_workspace_bytes(int B, int H, int T);
 int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out, const int32_t* beam_ids,
                  const int32_t* context_lens, int B, int H, int D, int T,
@@ -396,7 +397,9 @@ int llm_quantize_weights(const char* fp32_dir, const char* int8_dir, int num_lay
 /* Batched generate (CUDADecoder<T>::generate, decoder/cuda_decoder.cu:48-61,
  * batched): for each row, prompt tokens are consumed one per step (KV is
  * appended), then max_gen_len tokens are produced by greedy argmax.  out
- * [batch][max_gen_len] receives the generated ids (prompt excluded). */
+ * [batch][max_gen_len] receives the generated ids (prompt excluded).  A step
+ * whose fused o_proj clamped does not stop generation: `out` is filled to the
+ * end and LLM_ERR_RANGE is returned afterwards. */
 int llm_decoder_generate(llm_decoder* d, const int32_t* prompts, const int32_t* prompt_lens,
                          int prompt_stride, int batch, int max_gen_len, float temperature,
                          int32_t* out);
@@ -437,15 +440,19 @@ int llm_decoder_begin_beams(llm_decoder* d, int num_seqs, int beam_width, int sh
  * stream NULL -> the decoder's own stream. */
 int llm_decoder_step(llm_decoder* d, const int32_t* tokens, float* logits_dev,
                      int32_t* next_host, void* stream);
-/* Wait for the device.  LLM_ERR_RANGE if, since the last begin / generate, a
- * step's fused o_proj (FP16 decoders, LLM_PA_FORM_OPROJ) met a head product
- * outside its fixed-point range ((2^23 - 1) / num_heads in magnitude, or not
- * finite): that product was clamped, so the affected x values are wrong, but
- * the accumulator columns stayed consistent and later steps are unaffected by
- * it.  A step with next_host reports the same. */
+/* Wait for the device.  LLM_ERR_RANGE if, since the last report, a step's
+ * fused o_proj (FP16 decoders, LLM_PA_FORM_OPROJ) met a head product outside
+ * its fixed-point range ((2^23 - 1) / num_heads in magnitude, or not finite):
+ * that product was clamped, so the affected x values are wrong, but the
+ * accumulator columns stayed consistent and later steps are unaffected by it.
+ * A step with next_host reports the same.  Each clamp is reported once: the
+ * report clears the device flag, so later steps and syncs succeed unless they
+ * clamp again.  llm_decoder_run_attention launches carry a flag of their own
+ * and never make a step or a sync fail. */
 int llm_decoder_sync(llm_decoder* d);
 /* Health of the fused o_proj after waiting for the device: *clamped = 1 if a
- * term was clamped since the last begin / generate (see llm_decoder_sync),
+ * step's term was clamped since the last begin / generate, reported or not
+ * (see llm_decoder_sync),
  * *nonzero_columns = accumulator columns not back at zero (0 between steps
  * unless a launch was interrupted).  Either pointer may be NULL.  Decoders
  * without the fused o_proj report 0 / 0. */

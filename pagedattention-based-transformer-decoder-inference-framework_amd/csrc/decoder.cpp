@@ -94,14 +94,20 @@ struct llm_decoder {
   // attention launches: the adder completing a column clears it); oacc_run:
   // llm_decoder_run_attention's own set (allocated on first use), so a timed
   // run never mixes its arrivals with an in-flight step's; oflag: the range
-  // guard's device flag (common.hpp oacc_term), h_oflag its pinned host copy
+  // guard's device flag of the steps (common.hpp oacc_term), h_oflag its pinned
+  // host copy (written and read under mu only); oflag_run: run_attention's own
+  // flag, so a clamp in a timing re-run is never blamed on a step.
+  // range_clamped: a clamp was reported since the last begin / generate (what
+  // llm_decoder_oproj_status returns; the device flag is cleared on report)
   DevBuf<long long> oacc, oacc_run;
-  DevBuf<int> oflag;
+  DevBuf<int> oflag, oflag_run;
   int* h_oflag = nullptr;
+  int range_clamped = 0;
   // beam-group attention (row_group 4): the dynamic tile counters
   // (PaRowOutputs::beam_ctr), zero at create and left at zero by every launch
   DevBuf<unsigned> beam_ctr;
   int oproj_range_status();
+  int report_range(int flag);
   DevBuf<int32_t> tokens, pos, ctx;
   DevBuf<uint8_t> attn_ws;
   size_t attn_ws_bytes = 0;
@@ -401,6 +407,7 @@ struct Rows {
   // scratch row for llm_decoder_run_attention); no o_proj launch
   long long* oacc = nullptr;
   float* oproj_out = nullptr;
+  int* oflag = nullptr;  // the range guard's flag for these columns
 };
 
 // Activations feeding a weight GEMM (qa int8 / a16 fp16) are kept in packed-A
@@ -488,6 +495,7 @@ bool llm_decoder::oproj_fusable(const Rows& R) {
   Rows r = R;
   r.oacc = oacc.p;
   r.oproj_out = R.x;
+  r.oflag = oflag.p;
   PaPlan p;
   if (layer_attn(0, stream, r, &p) != LLM_OK) return false;
   return (p.form & LLM_PA_FORM_OPROJ) != 0;
@@ -528,7 +536,7 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
     ro.o_x = R.oproj_out;
     ro.wo_heads = wo_heads.p + (size_t)l * hid * hid;
     ro.o_n = hid;
-    ro.o_flag = oflag.p;
+    ro.o_flag = R.oflag;
     ro.out16 = tap_q ? R.act : nullptr;  // the taps read the packed o_proj input
   } else {
     ro.out16 = R.act;
@@ -671,7 +679,7 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
 // One decode step of all active rows (captured into the step graph).
 int llm_decoder::enqueue_step(hipStream_t st) {
   Rows R = step_rows(0, batch, attn_ws.p);
-  if (oproj_fusable(R)) R.oacc = oacc.p, R.oproj_out = R.x;
+  if (oproj_fusable(R)) R.oacc = oacc.p, R.oproj_out = R.x, R.oflag = oflag.p;
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -731,22 +739,32 @@ int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t
     if (oflag.p)
       LLM_HIP_RET(hipMemcpyAsync(h_oflag, oflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
     LLM_HIP_RET(hipStreamSynchronize(st));
-    if (oflag.p && *h_oflag) return oproj_range_status();
+    if (oflag.p) return report_range(*h_oflag);
   }
   return LLM_OK;
 }
 
-// LLM_ERR_RANGE once the fused o_proj's range flag is set (common.hpp
-// oacc_term); the flag stays set until reset_rows.
+// The fused o_proj's range guard (common.hpp oacc_term), reported ONCE: a set
+// flag returns LLM_ERR_RANGE and is cleared, so the steps after it (and the
+// next llm_decoder_sync) succeed unless they clamp again.  range_clamped keeps
+// the fact for llm_decoder_oproj_status until the next begin / generate.
+// Caller holds mu, with the steps' device work complete.
+int llm_decoder::report_range(int flag) {
+  if (!flag) return LLM_OK;
+  range_clamped = 1;
+  LLM_HIP_RET(hipMemsetAsync(oflag.p, 0, sizeof(int), stream));
+  LLM_HIP_RET(hipStreamSynchronize(stream));
+  return fail(LLM_ERR_RANGE,
+              "decoder: a head product of the fused o_proj left its fixed-point range "
+              "(|v| > (2^23 - 1) / num_heads, or not finite) and was clamped; the affected "
+              "hidden values of that step are wrong");
+}
+
 int llm_decoder::oproj_range_status() {
   if (!oflag.p) return LLM_OK;
-  LLM_HIP_RET(hipMemcpy(h_oflag, oflag.p, sizeof(int), hipMemcpyDeviceToHost));
-  if (*h_oflag)
-    return fail(LLM_ERR_RANGE,
-                "decoder: a head product of the fused o_proj left its fixed-point range "
-                "(|v| > (2^23 - 1) / num_heads, or not finite) and was clamped; the affected "
-                "hidden values of that step are wrong");
-  return LLM_OK;
+  int f = 0;
+  LLM_HIP_RET(hipMemcpy(&f, oflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  return report_range(f);
 }
 
 // Chunked prefill of `n` prompt tokens of active row `row` (the reference's
@@ -842,6 +860,7 @@ static int reset_rows(llm_decoder* d, int batch, int start_pos) {
   for (int b = 0; b < batch; ++b) d->h_pos[b] = start_pos;
   if (d->oacc.p) LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * d->oacc.n));
   if (d->oflag.p) LLM_HIP_RET(hipMemset(d->oflag.p, 0, sizeof(int)));
+  d->range_clamped = 0;
   std::vector<int32_t> pos(batch, start_pos), ctx(batch, start_pos + 1), tok(batch, 0);
   LLM_HIP_RET(hipMemcpy(d->pos.p, pos.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
   LLM_HIP_RET(hipMemcpy(d->ctx.p, ctx.data(), sizeof(int32_t) * batch, hipMemcpyHostToDevice));
@@ -952,7 +971,7 @@ extern "C" int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form
   std::lock_guard<std::mutex> g(d->mu);
   LLM_REQUIRE(d->batch > 0, "llm_decoder_attention_plan: no active rows");
   Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
-  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.x;
+  if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.x, R.oflag = d->oflag.p;
   PaPlan p;
   RET_IF(d->layer_attn(0, d->stream, R, &p));
   *nsplit = p.nsplit;
@@ -969,13 +988,16 @@ extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream
   Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
   // the step's fused o_proj writes the attention rows' fp32 buffer here, not
   // x, and accumulates into columns of its own (oacc_run: zero at allocation,
-  // and every completed column clears itself, as the step's do)
+  // and every completed column clears itself, as the step's do) with a range
+  // flag of its own (oflag_run: a clamp here never fails a step or a sync)
   if (d->oproj_fusable(R)) {
     if (!d->oacc_run.p) {
       RET_IF(d->oacc_run.alloc(d->oacc.n));
       LLM_HIP_RET(hipMemset(d->oacc_run.p, 0, sizeof(long long) * d->oacc_run.n));
+      RET_IF(d->oflag_run.alloc(1));
+      LLM_HIP_RET(hipMemset(d->oflag_run.p, 0, sizeof(int)));
     }
-    R.oacc = d->oacc_run.p, R.oproj_out = R.o;
+    R.oacc = d->oacc_run.p, R.oproj_out = R.o, R.oflag = d->oflag_run.p;
   }
   return d->layer_attn(layer, st, R);
 }
@@ -987,6 +1009,7 @@ extern "C" int llm_decoder_oproj_status(llm_decoder* d, int* clamped, long long*
   int f = 0;
   long long nz = 0;
   if (d->oflag.p) LLM_HIP_RET(hipMemcpy(&f, d->oflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  f = f || d->range_clamped;
   for (const DevBuf<long long>* b : {&d->oacc, &d->oacc_run}) {
     if (!b->p) continue;
     std::vector<long long> h(b->n);
@@ -1019,6 +1042,7 @@ extern "C" int llm_decoder_copy_next(llm_decoder* d, int32_t* dst_dev, void* str
 extern "C" int llm_decoder_sync(llm_decoder* d) {
   LLM_REQUIRE(d, "llm_decoder_sync: NULL");
   LLM_HIP_RET(hipDeviceSynchronize());
+  std::lock_guard<std::mutex> g(d->mu);
   return d->oproj_range_status();
 }
 
@@ -1071,13 +1095,21 @@ extern "C" int llm_decoder_generate(llm_decoder* d, const int32_t* prompts,
   for (int b = 0; b < batch; ++b)
     if (prompt_lens[b] > 1)
       RET_IF(d->prefill(b, prompts + (size_t)b * prompt_stride, prompt_lens[b] - 1, d->stream));
+  // a step whose fused o_proj clamped (LLM_ERR_RANGE) still produced its ids:
+  // generation runs to the end, fills `out`, and then returns the status
   std::vector<int32_t> tok(batch), next(batch);
+  int range_rc = LLM_OK;
   for (int s = 0; s < max_gen_len; ++s) {
     for (int b = 0; b < batch; ++b)
       tok[b] = s == 0 ? prompts[(size_t)b * prompt_stride + prompt_lens[b] - 1] : next[b];
-    RET_IF(d->run_step(tok.data(), nullptr, next.data(), d->stream));
+    const int rc = d->run_step(tok.data(), nullptr, next.data(), d->stream);
+    if (rc == LLM_ERR_RANGE) range_rc = rc;
+    else RET_IF(rc);
     for (int b = 0; b < batch; ++b) out[(size_t)b * max_gen_len + s] = next[b];
   }
+  if (range_rc) return fail(LLM_ERR_RANGE, "llm_decoder_generate: the fused o_proj clamped a head "
+                                           "product in at least one step; `out` is complete, the "
+                                           "ids after that step may differ");
   return LLM_OK;
 }
 

@@ -3,10 +3,8 @@
 // pa_decode_grouped, pa_decode_plan).  The split kernel itself, and the design
 // notes of the scan, are in pa_split.hpp; the tuning build's experiment
 // kernels and A/B entry are in csrc/tune/pa_decode_tune.hip.
-#include "pa_beam_steal.hpp"
-#if LLM_TUNING
-#include "tune/pa_decode_tune.hpp"
-#endif
+#include "pa_split.hpp"
+#include "pa_tuning.hpp"
 
 namespace llm {
 
@@ -268,100 +266,22 @@ long long resident_waves() {
   return cached;
 }
 
-// The MFMA beam-group kernel (pa_beam_mfma_kernel, LLM_BEAM_MFMA=1) and the
-// one-wave-per-beam-group kernel (pa_beam4_kernel, LLM_BEAM4=1; LLM_BEAM4_SPLITS
-// forces its split count) exist only in the tuning build
-// (csrc/tune/pa_decode_tune.hip).  Both measured slower than the LDS-staged BEAM
-// form of pa_split_kernel (C4 launch with merge: beam4 69.2 us at 16 splits,
-// 74.2 with two pages per register stage, 82.3 at 12 splits, against 67.6 us;
-// MFMA 69.8 vs 60.8 us).
-bool beam4_on() {
-#if LLM_TUNING
-  return env_int("LLM_BEAM4", 0) != 0;  // read per launch
-#else
-  return false;
-#endif
-}
-
-long long beam4_resident_for(int D, int TS) {
-#if LLM_TUNING
-  return tune_beam4_resident_for(D, TS);
-#else
-  (void)D, (void)TS;
-  return 0;
-#endif
-}
-
-bool beam_mfma_on() {
-#if LLM_TUNING
-  return env_int("LLM_BEAM_MFMA", 0) != 0;  // read per launch: a test sets and restores it
-#else
-  return false;
-#endif
-}
-// Workgroup-merge form of the fp16 row-output launch (PaSplitArgs::wgm); the
-// tuning build's LLM_WG_MERGE=0 restores split + merge launches (A/B, parity).
-bool wg_merge_on() {
-#if LLM_TUNING
-  return env_int("LLM_WG_MERGE", 1) != 0;  // read per launch: a test flips it in-process
-#else
-  return true;
-#endif
-}
 }  // namespace
+
 // The FP16 decoder's o_proj fused into the workgroup merge (decoder.cpp
-// oproj_fusable); the tuning build's LLM_OPROJ_FUSE=0 restores the o_proj
-// GEMM launch (A/B, parity).
-bool oproj_fuse_on() {
-#if LLM_TUNING
-  return env_int("LLM_OPROJ_FUSE", 1) != 0;
-#else
-  return true;
-#endif
-}
-bool beam_steal_on() {
-#if LLM_TUNING
-  return env_int("LLM_BEAM_STEAL", 0) == 1;  // read per launch
-#else
-  return false;
-#endif
-}
-// The steal form's exchange splits a shared page's 2 NI pieces of 1 KiB over
-// the 4 waves: NI = TS D / 512 even (fp16 pages of 2, 4 or 8 KiB).
-constexpr bool steal_shape_ok(int D, int TS) {
-  return D >= 8 && D <= 512 && (TS * D) % 1024 == 0 && TS * D * 2 <= 8192;
-}
-// Standalone beam launches (pa_decode C entry, no decoder-owned counters):
-// the tuning build's LLM_BEAM_STEAL=1 runs the steal form on counters of its
-// own (one buffer per process: launches must not overlap).
-unsigned* standalone_steal_counters(size_t n) {
-#if LLM_TUNING
-  static unsigned* buf = nullptr;
-  static size_t cap = 0;
-  if (env_int("LLM_BEAM_STEAL", 0) != 1) return nullptr;
-  if (n > cap) {
-    if (buf) (void)hipFree(buf);
-    buf = nullptr;
-    cap = 0;
-    if (hipMalloc(&buf, n * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemset(buf, 0, n * sizeof(unsigned)) != hipSuccess) return nullptr;
-    cap = n;
-  }
-  return buf;
-#else
-  (void)n;
-  return nullptr;
-#endif
-}
+// oproj_fusable); LLM_OPROJ_FUSE=0 (tuning build) restores the o_proj GEMM.
+bool oproj_fuse_on() { return pa_tuning().oproj_fuse; }
+bool beam_steal_on() { return pa_tuning().beam_steal; }
+
 namespace {
-int beam_mfma_balance16() {
-#if LLM_TUNING
-  static const int v = env_int("LLM_BEAM_MFMA_BALANCE16", 64);
-  return v >= 16 ? v : 0;
-#else
-  return 64;
-#endif
-}
+
+// The experiment forms of beam-group launches (pa_beam4_kernel,
+// pa_beam_mfma_kernel, the steal form, ...) exist only in the tuning build
+// (csrc/tune/pa_decode_tune.hip, switched by pa_tuning.hpp).  All measured
+// slower than the LDS-staged BEAM form of pa_split_kernel (C4 launch with
+// merge: beam4 69.2 us at 16 splits, 74.2 with two pages per register stage,
+// 82.3 at 12 splits, against 67.6 us; MFMA 69.8 vs 60.8 us; steal 76-92 vs
+// 65.3 us).
 
 template <int D, int TS, int KVT>
 hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool* beam) {
@@ -393,34 +313,6 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
                        dim3(a.B * a.H), dim3(64 * a.nsplit), 0, st, a);
     return hipGetLastError();
   }
-#if LLM_TUNING
-  if (a.group == 4 && !direct && ST == 2 && a.beam4) {
-    // pa_beam4_kernel: one wave per (group, head, split)
-    *beam = true;
-    return tune_launch_beam4(a, D, TS, st);
-  }
-#endif
-#if LLM_TUNING
-  if (a.group == 4 && !direct && a.steal) {  // dynamic tile assignment (pa_beam_steal.hpp)
-    if constexpr (steal_shape_ok(D, TS)) {
-      if constexpr (D == 128 && TS == 16) {
-        if (env_int("LLM_BEAM_STAMPS", 0) == 1) {  // per-wave timestamps (scripts/beam_stamps.py)
-          *beam = true;
-          return tune_launch_steal_stamps(a, grid, st);
-        }
-      }
-      const int kb = env_int("LLM_STEAL_KB", kStealBatch);  // tuning: tiles per batch
-      if (env_int("LLM_STEAL_MINW", 0) == 3)  // tuning: no 128-VGPR cap (3 waves per SIMD)
-        hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, kStealBatch, 3>), grid, block, 0, st, a);
-      else if (kb == 2) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 2>), grid, block, 0, st, a);
-      else if (kb == 8) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 8>), grid, block, 0, st, a);
-      else if (kb == 16) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 16>), grid, block, 0, st, a);
-      else hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS>), grid, block, 0, st, a);
-      *beam = true;
-      return hipGetLastError();
-    }
-  }
-#endif
   if (a.group == 4 && !direct && ST == 2) {
     // 8 KiB register stages: 112 VGPRs, 4 waves per SIMD.  The 16 KiB form
     // (179 VGPRs, 2 waves) spent 27 % of its wave time in issue stalls and
@@ -430,29 +322,11 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
 #define LLM_BEAM_CHUNK 8192
 #define LLM_BEAM_WAVES 0
 #endif
-#if LLM_TUNING
-    if constexpr (D == 128 && TS == 16) {
-      if (beam_mfma_on()) {
-        PaSplitArgs am = a;
-        am.balance16 = beam_mfma_balance16();
-        *beam = true;
-        return tune_launch_beam_mfma(am, grid, st);
-      }
-      if (env_int("LLM_BEAM_DIAG", 0) == 1) {  // this form's loads, staging and barriers only
-        *beam = true;
-        return tune_launch_beam_loads_only(a, grid, st);
-      }
-      if (env_int("LLM_BEAM_STAMPS", 0) == 1) {  // per-wave timestamps (scripts/beam_stamps.py)
-        *beam = true;
-        return tune_launch_beam_stamps(a, grid, st);
-      }
-      const int ring = env_int("LLM_BEAM_RING", 0);
-      if (ring > 0) {  // shared chunks through an LDS-DMA ring
-        *beam = true;
-        return tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
-      }
+    hipError_t te;
+    if (tune_launch_form(a, D, TS, grid, st, &te)) {  // tuning build: an experiment form
+      *beam = true;
+      return te;
     }
-#endif
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
                                         false, true>), grid, block, 0, st, a);
     *beam = true;
@@ -644,27 +518,10 @@ int llm::pa_merge_rows_internal(const float* part_acc, const float* part_ml, flo
 }
 
 namespace {
-// Cost of a beam-private tile relative to a shared one, in 1/16ths (beam-group
-// launches, dynamic splits).  In the tuning build (make tune) LLM_BEAM_BALANCE16
-// overrides it (0: equal tile counts, the plain partition).
-int beam_balance16() {
-#if LLM_TUNING
-  static const int v = [] {
-    const char* e = std::getenv("LLM_BEAM_BALANCE16");
-    const int x = e ? std::atoi(e) : 44;
-    return x >= 16 ? x : 0;
-  }();
-  return v;
-#else
-  return 44;  // measured sweep in DESIGN.md §8 (C4 launch 84 -> 66 us)
-#endif
-}
-
 template <int D, int TS>
 hipError_t beam_occupancy(int* blocks) {
-#if LLM_TUNING
-  if (D == 128 && TS == 16 && beam_mfma_on()) return tune_beam_mfma_occupancy(blocks);
-#endif
+  hipError_t e;
+  if (tune_beam_occupancy(D, TS, blocks, &e)) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(
       blocks, pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true>,
       256, 0);
@@ -761,8 +618,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // resident waves (2 / 4 / 8 waves per workgroup: a 6-wave workgroup would
   // leave 2 of the 8 slots idle): C3 6 -> 8 splits
   const bool f32_rows = rows && rows->f32_rows && !rows->q && !rows->out16;
+  const PaTuning tn = pa_tuning();
   const bool wgm_ok = ((row_out && rows->out16 && !rows->q) || oproj || f32_rows) && row_group == 1 &&
-                      kv->kv_dtype == LLM_F16 && wg_merge_on();
+                      kv->kv_dtype == LLM_F16 && tn.wg_merge;
   int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident_launch);
   if (wgm_ok && pps_fixed <= 0 && !f32_rows) {
     const int nw = choose_nsplit(B, H, ntiles_max, 0, resident_launch, kWgmShortPps);
@@ -773,35 +631,29 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     while (nw < nsplit && nw < kWgmMaxSplits) nw *= 2;
     if (nw >= nsplit && (long long)nw * kMaxPps >= ntiles_max) nsplit = nw;
   }
-#if LLM_TUNING
-  // tuning build: LLM_BEAM_NSPLIT forces the split count of beam-group launches
+  // tuning build: forced split counts of beam-group launches and of the
+  // workgroup-merge eligible ones (fp16 row outputs, dynamic splits)
   if (row_group == 4 && pps_fixed <= 0) {
-    const int f = env_int("LLM_BEAM_NSPLIT", 0);
+    const int f = tn.beam_nsplit;
     if (f >= 2 && (long long)f * kMaxPps >= ntiles_max) nsplit = std::min(f, kMaxSplits);
   }
-  // tuning build: LLM_WGM_SPLITS forces the split count of workgroup-merge
-  // eligible launches (fp16 row outputs, dynamic splits)
   if (rows && (rows->out16 || oproj) && !rows->q && row_group == 1 && pps_fixed <= 0) {
-    const int f = env_int("LLM_WGM_SPLITS", 0);
+    const int f = tn.wgm_splits;
     if (f >= 2 && f <= kWgmMaxSplits && (long long)f * kMaxPps >= ntiles_max) nsplit = f;
   }
-#endif
   // beam groups of 4 rows (fp16 pages <= 8 KiB, dynamic splits): pa_beam4_kernel,
   // one wave per (group, head, split), splits sized for its own occupancy (a
   // whole number of resident rounds over (group, head) pairs), each split
   // holding <= 128 page items; fixed pages_per_split keeps the BEAM form
   bool use_beam4 = false;
   if (row_group == 4 && pps_fixed <= 0 && kv->kv_dtype == LLM_F16 && TS * D * 2 <= 8192 &&
-      beam4_on() && !beam_mfma_on()) {
+      tn.beam4 && !tn.beam_mfma) {
     const long long groups = (long long)((B + 3) / 4) * H;
     const long long need = (4LL * ntiles_max + kMaxPps - 1) / kMaxPps;
-    long long ns = (beam4_resident_for(D, TS) + groups - 1) / groups;
+    long long ns = (tune_beam4_resident_for(D, TS) + groups - 1) / groups;
     ns = std::max(std::max(ns, need), 2LL);
     ns = std::min(ns, max_nsplit(B, H, ntiles_max));
-#if LLM_TUNING
-    const int f = env_int("LLM_BEAM4_SPLITS", 0);
-    if (f >= 2) ns = std::min<long long>(f, max_nsplit(B, H, ntiles_max));
-#endif
+    if (tn.beam4_splits >= 2) ns = std::min<long long>(tn.beam4_splits, max_nsplit(B, H, ntiles_max));
     if (ns >= need && ns >= 2) {
       use_beam4 = true;
       nsplit = (int)ns;
@@ -813,9 +665,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
                 "pages_per_split, or pass 0; T <= 16384 pages)");
   const bool direct = nsplit <= 1;
   // beam groups of 4 fp16 rows with counters: dynamic tile assignment
-  const bool steal_form = row_group >= 4 && !direct && kv->kv_dtype == LLM_F16 &&
-                          pps_fixed <= 0 && !use_beam4 && !beam_mfma_on() &&
-                          steal_shape_ok(D, TS);
+  const bool steal_form = tn.beam_steal && row_group >= 4 && !direct &&
+                          kv->kv_dtype == LLM_F16 && pps_fixed <= 0 && !use_beam4 &&
+                          !tn.beam_mfma && steal_shape_ok(D, TS);
   if (plan) {
     const int group = std::max(1, std::min(row_group, 4));
     const bool wg = wgm_ok && !direct && group == 1 && nsplit <= kWgmMaxSplits;
@@ -830,9 +682,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     return LLM_OK;
   }
   unsigned* steal_ctr = nullptr;
-  if (steal_form && LLM_TUNING)
+  if (steal_form)
     steal_ctr = rows && rows->beam_ctr ? rows->beam_ctr
-                                       : standalone_steal_counters(2 * (size_t)((B + 3) / 4) * H);
+                                       : tune_steal_counters(2 * (size_t)((B + 3) / 4) * H);
   LLM_REQUIRE(!direct || out != nullptr, "pa_decode: single-split launch needs the fp32 out");
   if (oproj && (direct || row_group != 1 || nsplit > kWgmMaxSplits || !wgm_ok))
     return fail(LLM_ERR_UNSUPPORTED, "pa_decode: the fused o_proj needs the workgroup-merge form");
@@ -865,7 +717,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     a.part_acc = static_cast<float*>(workspace);
     a.part_ml = a.part_acc + (size_t)B * H * nsplit * D;
   }
-  a.balance16 = beam_balance16();
+  a.balance16 = tn.beam_balance16;
   a.beam4 = use_beam4 ? 1 : 0;
   a.steal = a.group == 4 ? steal_ctr : nullptr;
   if (wgm) {

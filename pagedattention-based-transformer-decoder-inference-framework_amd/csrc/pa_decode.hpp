@@ -38,7 +38,7 @@ struct PaRowOutputs {
   int* o_flag = nullptr;
   // Beam-group launches (row_group 4, fp16 KV): 2 * ceil(B / 4) * H counters,
   // zero before the first launch and left at zero by every launch; with them
-  // the launch assigns tiles dynamically (pa_beam_steal.hpp,
+  // the launch assigns tiles dynamically (csrc/tune/pa_beam_steal.hpp,
   // LLM_PA_FORM_STEAL), without them it runs the static BEAM form
   unsigned* beam_ctr = nullptr;
 };
@@ -64,7 +64,7 @@ int pa_pages_per_split(int B, int H, int T, int TS, int max_tiles);
 bool oproj_fuse_on();
 
 // Whether the decoder's beam launches assign tiles while they run
-// (PaRowOutputs::beam_ctr, pa_beam_steal.hpp): tuning build, LLM_BEAM_STEAL=1
+// (PaRowOutputs::beam_ctr, csrc/tune/pa_beam_steal.hpp): tuning build, LLM_BEAM_STEAL=1
 // (same-box it lost to the static BEAM form).
 bool beam_steal_on();
 

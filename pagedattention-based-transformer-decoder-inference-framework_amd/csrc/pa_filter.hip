@@ -236,7 +236,10 @@ __global__ __launch_bounds__(kFilterThreads) void pa_filter_kernel(PaFilterArgs 
 using namespace llm;
 
 namespace {
-int filter_row_stride(int T) {  // the bitonic sort's power-of-two length
+// The longest row the filtered form takes: its power-of-two sort length must
+// stay an int (filter_row_stride), and 2^30 tokens is far past any context
+constexpr int kFilterRowMaxT = 1 << 30;
+int filter_row_stride(int T) {  // the bitonic sort's power-of-two length, T <= kFilterRowMaxT
   int Tp = 1;
   while (Tp < T) Tp <<= 1;
   return Tp;
@@ -244,7 +247,7 @@ int filter_row_stride(int T) {  // the bitonic sort's power-of-two length
 }  // namespace
 
 extern "C" size_t pa_decode_ex_workspace_bytes(int B, int H, int T) {
-  if (B <= 0 || H <= 0 || T <= kFilterMaxT) return 0;
+  if (B <= 0 || H <= 0 || T <= kFilterMaxT || T > kFilterRowMaxT) return 0;
   return (size_t)B * H * filter_row_stride(T) * (sizeof(uint64_t) + sizeof(float));
 }
 
@@ -275,6 +278,8 @@ extern "C" int pa_decode_ex(const pa_kv_view* kv, const float* q, float* out,
                    kv->page_stride % 16 == 0),
               "pa_decode_ex: page_stride must be 0 or >= one page and a multiple of 16");
   if (D > 256) return fail(LLM_ERR_UNSUPPORTED, "pa_decode_ex: filters / weight outputs need D <= 256");
+  if (T > kFilterRowMaxT)
+    return fail(LLM_ERR_UNSUPPORTED, "pa_decode_ex: filters / weight outputs need T <= 2^30");
   const bool ws_form = T > kFilterMaxT;
   const size_t need = pa_decode_ex_workspace_bytes(B, H, T);
   LLM_REQUIRE(!ws_form || (workspace != nullptr && workspace_bytes >= need &&

@@ -88,7 +88,7 @@ struct PaSplitArgs {
   const _Float16* wo_heads;  // [H][D/8][o_n][8]
   int o_n;
   int* o_flag;  // set to 1 when a head's term was clamped (common.hpp oacc_term)
-  // beam-group launches with dynamic tile assignment (pa_beam_steal.hpp):
+  // beam-group launches with dynamic tile assignment (tuning build, tune/pa_beam_steal.hpp):
   // per (sequence group, head) the next-batch counter and the arrival count,
   // zero at launch, left at zero by the launch
   unsigned* steal;

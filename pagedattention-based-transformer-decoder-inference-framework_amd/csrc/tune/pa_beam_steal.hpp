@@ -1,5 +1,7 @@
-// Beam-group attention with dynamic tile assignment (the C4 decode launch;
-// device code of pa_decode.hip, form LLM_PA_FORM_STEAL).
+// Beam-group attention with dynamic tile assignment (tuning build only:
+// csrc/tune/pa_decode_tune.hip, LLM_BEAM_STEAL=1, plan form LLM_PA_FORM_STEAL).
+// Measured slower than the shipped static BEAM form at every batch size
+// (C4 launch 76.1-92.2 vs 65.3 us); kept for A/Bs.
 //
 // Same work as pa_split_kernel's BEAM form (one workgroup = the 4 beams of one
 // sequence for one (head, split), wave i = beam i; a tile whose page id is the

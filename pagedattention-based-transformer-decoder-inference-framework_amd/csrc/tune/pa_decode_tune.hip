@@ -1,12 +1,14 @@
 // Tuning build only (make tune -> libllm_decoder_hip_tune.so; never in
 // libllm_decoder_hip.so): the beam-group attention experiments that measured
 // slower than the shipped BEAM form of pa_split_kernel, the
-// hooks pa_decode.hip calls when they are switched on (LLM_BEAM4,
-// LLM_BEAM_MFMA), and the pa_decode_tune A/B entry of the split kernel's
-// register-stage / cache-policy variants (scripts/bench_kernels.py,
+// tuning table pa_decode.hip reads (pa_tuning.hpp: the switches from the
+// environment, and tune_launch_form, which routes a beam-group launch to the
+// experiment switched on), and the pa_decode_tune A/B entry of the split
+// kernel's register-stage / cache-policy variants (scripts/bench_kernels.py,
 // scripts/tune_attention.py).
 #include "tune/pa_decode_tune.hpp"
-#include "pa_beam_steal.hpp"
+#include "tune/pa_beam_steal.hpp"
+#include "pa_tuning.hpp"
 
 namespace llm {
 
@@ -834,6 +836,111 @@ hipError_t tune_launch_steal_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_
 
 hipError_t tune_beam_mfma_occupancy(int* blocks) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, pa_beam_mfma_kernel<0>, 256, 0);
+}
+
+// ---------------------------------------------------------------------------
+// The tuning table (pa_tuning.hpp): every switch read per launch (tests flip
+// them in-process), except the beam balance, read once.
+PaTuning pa_tuning() {
+  static const int balance = [] {
+    const int x = env_int("LLM_BEAM_BALANCE16", 44);
+    return x >= 16 ? x : 0;
+  }();
+  static const int mfma_balance = [] {
+    const int x = env_int("LLM_BEAM_MFMA_BALANCE16", 64);
+    return x >= 16 ? x : 0;
+  }();
+  PaTuning t;
+  t.wg_merge = env_int("LLM_WG_MERGE", 1) != 0;
+  t.oproj_fuse = env_int("LLM_OPROJ_FUSE", 1) != 0;
+  t.beam4 = env_int("LLM_BEAM4", 0) != 0;
+  t.beam_mfma = env_int("LLM_BEAM_MFMA", 0) != 0;
+  t.beam_steal = env_int("LLM_BEAM_STEAL", 0) == 1;
+  t.beam_balance16 = balance;
+  t.beam_mfma_balance16 = mfma_balance;
+  t.beam_nsplit = env_int("LLM_BEAM_NSPLIT", 0);
+  t.wgm_splits = env_int("LLM_WGM_SPLITS", 0);
+  t.beam4_splits = env_int("LLM_BEAM4_SPLITS", 0);
+  return t;
+}
+
+bool tune_beam_occupancy(int D, int TS, int* blocks, hipError_t* e) {
+  if (D != 128 || TS != 16 || !pa_tuning().beam_mfma) return false;
+  *e = tune_beam_mfma_occupancy(blocks);
+  return true;
+}
+
+unsigned* tune_steal_counters(size_t n) {
+  static unsigned* buf = nullptr;
+  static size_t cap = 0;
+  if (!pa_tuning().beam_steal) return nullptr;
+  if (n > cap) {
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipMalloc(&buf, n * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(buf, 0, n * sizeof(unsigned)) != hipSuccess) return nullptr;
+    cap = n;
+  }
+  return buf;
+}
+
+namespace {
+// the steal form (pa_beam_steal_kernel) of one (D, TS): LLM_STEAL_KB tiles per
+// batch, LLM_STEAL_MINW=3 lifts the 128-VGPR cap, LLM_BEAM_STAMPS=1 stamps
+template <int D, int TS>
+hipError_t launch_steal(const PaSplitArgs& a, dim3 grid, hipStream_t st) {
+  if constexpr (D == 128 && TS == 16) {
+    if (env_int("LLM_BEAM_STAMPS", 0) == 1) return tune_launch_steal_stamps(a, grid, st);
+  }
+  const int kb = env_int("LLM_STEAL_KB", kStealBatch);
+  if (env_int("LLM_STEAL_MINW", 0) == 3)
+    hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, kStealBatch, 3>), grid, dim3(256), 0, st, a);
+  else if (kb == 2) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 2>), grid, dim3(256), 0, st, a);
+  else if (kb == 8) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 8>), grid, dim3(256), 0, st, a);
+  else if (kb == 16) hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS, 16>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((pa_beam_steal_kernel<D, TS>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+}  // namespace
+
+bool tune_launch_form(const PaSplitArgs& a, int D, int TS, dim3 grid, hipStream_t st,
+                      hipError_t* e) {
+  if (a.beam4) {  // pa_beam4_kernel: one wave per (group, head, split)
+    *e = tune_launch_beam4(a, D, TS, st);
+    return true;
+  }
+  if (a.steal && steal_shape_ok(D, TS)) {  // dynamic tile assignment (pa_beam_steal.hpp)
+    if (D == 64 && TS == 16) *e = launch_steal<64, 16>(a, grid, st);
+    else if (D == 128 && TS == 16) *e = launch_steal<128, 16>(a, grid, st);
+    else if (D == 32 && TS == 32) *e = launch_steal<32, 32>(a, grid, st);
+    else if (D == 64 && TS == 32) *e = launch_steal<64, 32>(a, grid, st);
+    else if (D == 128 && TS == 32) *e = launch_steal<128, 32>(a, grid, st);
+    else return false;
+    return true;
+  }
+  if (D != 128 || TS != 16) return false;
+  const PaTuning t = pa_tuning();
+  if (t.beam_mfma) {
+    PaSplitArgs am = a;
+    am.balance16 = t.beam_mfma_balance16;
+    *e = tune_launch_beam_mfma(am, grid, st);
+    return true;
+  }
+  if (env_int("LLM_BEAM_DIAG", 0) == 1) {  // this form's loads, staging and barriers only
+    *e = tune_launch_beam_loads_only(a, grid, st);
+    return true;
+  }
+  if (env_int("LLM_BEAM_STAMPS", 0) == 1) {  // per-wave timestamps (scripts/beam_stamps.py)
+    *e = tune_launch_beam_stamps(a, grid, st);
+    return true;
+  }
+  const int ring = env_int("LLM_BEAM_RING", 0);
+  if (ring > 0) {  // shared chunks through an LDS-DMA ring
+    *e = tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
+    return true;
+  }
+  return false;
 }
 
 }  // namespace llm

@@ -189,14 +189,15 @@ class ShardedDecode:
 
 def timed_run(sd: ShardedDecode, warmup: int, steps: int, first_tokens, *,
               sync: Callable[[], None] | None = None, timer_device="cuda",
-              step_times: list | None = None) -> float:
+              step_times: list | None = None, rank_times: list | None = None) -> float:
     """bench.py's measured loop: `warmup` untimed steps (the first feeds
     first_tokens, later steps feed back the device's ids), then exactly `steps`
     timed ones bracketed by a barrier + device synchronisation on both sides.
     Returns the elapsed seconds, the MAX over ranks.  step_times (a list, GPU
     ranks only): filled with this rank's per-step device times in seconds,
     from HIP events recorded on torch's current stream (the stream the steps
-    run on) between consecutive steps."""
+    run on) between consecutive steps.  rank_times (a list): filled with every
+    rank's own elapsed seconds, in rank order (one entry in a single process)."""
     import torch
     import torch.distributed as dist
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -227,11 +228,44 @@ def timed_run(sd: ShardedDecode, warmup: int, steps: int, first_tokens, *,
     elapsed = time.perf_counter() - t0
     if ev:
         step_times[:] = [ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(steps)]
+    per_rank = [elapsed]
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device=timer_device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed
+        ts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(ts, t)
+        per_rank = [float(x.item()) for x in ts]
+    if rank_times is not None:
+        rank_times[:] = per_rank
+    return max(per_rank)
+
+
+def time_gather(sd: ShardedDecode, iters: int = 10, *, sync: Callable[[], None] | None = None,
+                timer_device="cuda") -> float | None:
+    """Seconds one step's gather takes on its own (no decode step beside it):
+    `iters` back-to-back gathers of the step buffer, barrier + sync on both
+    sides, the MAX over ranks.  None when this loop gathers nothing."""
+    import torch
+    import torch.distributed as dist
+    if sd.g is None or sd.world == 1:
+        return None
+    if sync is None:
+        sync = torch.cuda.synchronize
+    g = sd.g
+    buf, recv = g.bufs[0], g.recv[0]
+    _gather(buf, recv, g.rank, g.equal).wait()  # warm the communicator's path
+    sync()
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        _gather(buf, recv, g.rank, g.equal).wait()
+    sync()
+    dist.barrier()
+    sync()
+    t = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64,
+                     device=timer_device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def distributed_generate(make_decoder: Callable, prompts: Sequence[Sequence[int]],

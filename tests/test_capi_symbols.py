@@ -95,6 +95,15 @@ def test_invalid_arguments_rejected_before_any_launch():
     assert lib.pa_decode_ex_workspace_bytes(1, 1, 8193) == 16384 * 12
     assert lib.pa_decode_ex_workspace_bytes(3, 2, 20000) == 3 * 2 * 32768 * 12
     assert lib.pa_decode_ex_workspace_bytes(0, 2, 20000) == 0
+    # rows past 2^30 tokens are refused up front (the sort length would overflow
+    # an int), never a hang in the power-of-two search
+    assert lib.pa_decode_ex_workspace_bytes(1, 1, (1 << 30) + 1) == 0
+    assert lib.pa_decode_ex_workspace_bytes(1, 1, 2**31 - 1) == 0
+    assert lib.pa_decode_ex_workspace_bytes(1, 1, 1 << 30) == (1 << 30) * 12
+    huge = exargs[:7] + (2**31 - 1,)
+    assert lib.pa_decode_ex(ctypes.byref(fake), *huge, ctypes.byref(opt), ctypes.c_void_p(8),
+                            1 << 62, None) == llm_capi.LLM_ERR_UNSUPPORTED
+    assert b"T <= 2^30" in lib.llm_last_error()
     # pa_prefill: NULL view / q / out, unsupported pools (int8) and positions
     # past the page table are rejected on the host
     assert lib.pa_prefill(None, None, 0, None, 0, 0, 0, 1, 1.0, None, 0, None) == 1

@@ -167,11 +167,14 @@ def test_fused_oproj(gpu, ctx, H, D, ts):
         assert np.mean(fa != fg) < 0.05, np.mean(fa != fg)
 
 
-def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3):
+def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3, after=None):
     """Fused-o_proj range guard runs (tuning build, forced split count, context
     0 so each row's attention output is exactly its new V row): per step the
     logits, llm_decoder_sync's status, then llm_decoder_oproj_status, and the
-    step-0 taps (uint16 [L][4][B16 * qa_ld])."""
+    step-0 taps (uint16 [L][4][B16 * qa_ld]).  Every step's sync is followed by
+    a second one, whose status must be LLM_OK (a clamp is reported once).
+    after(lib, dec): called on the decoder after the steps (its result is
+    returned last)."""
     import torch
     import llm_capi
     os.environ["LLM_WGM_SPLITS"] = str(splits)
@@ -183,6 +186,7 @@ def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3):
                        ("llm_decoder_step", [ctypes.c_void_p] * 5),
                        ("llm_decoder_sync", [ctypes.c_void_p]),
                        ("llm_decoder_set_taps", [ctypes.c_void_p] * 3),
+                       ("llm_decoder_oproj_status", [ctypes.c_void_p] * 3),
                        ("llm_decoder_destroy", [ctypes.c_void_p])):
         getattr(lib, name).argtypes = args
     lib.llm_decoder_destroy.restype = None
@@ -206,13 +210,15 @@ def _guard_run(lib, w, L, H, D, V, B, steps, fuse, splits=3):
             llm_capi.check(lib.llm_decoder_step(dec, tok.ctypes.data, logits.data_ptr(), None, None),
                            lib)
             rcs.append(lib.llm_decoder_sync(dec))
+            assert lib.llm_decoder_sync(dec) == 0  # reported once, then cleared
             out.append(logits.cpu().numpy().copy())
             if s == 0:
                 taps = tq.cpu().numpy().view(np.uint16).copy()
                 llm_capi.check(lib.llm_decoder_set_taps(dec, None, None), lib)
         clamped, nz = ctypes.c_int(-1), ctypes.c_longlong(-1)
         llm_capi.check(lib.llm_decoder_oproj_status(dec, ctypes.byref(clamped), ctypes.byref(nz)), lib)
-        return np.stack(out), rcs, (clamped.value, nz.value), taps
+        res = (np.stack(out), rcs, (clamped.value, nz.value), taps)
+        return res + (after(lib, dec),) if after else res
     finally:
         lib.llm_decoder_destroy(dec)
         os.environ.pop("LLM_WGM_SPLITS", None)
@@ -272,5 +278,34 @@ def test_fused_oproj_range_guard(gpu):
     wn["wqkv"] = w["wqkv"].copy()
     wn["wqkv"][0, :, 2 * hid:] = (3000 * rng.standard_normal((hid, hid))).astype(np.float16)
     wn = {k: np.ascontiguousarray(v) for k, v in wn.items()}
-    _, frc, fst, _ = _guard_run(tune, wn, L, H, D, V, B, 2, fuse=True)
+    _, frc, fst, _, (gen_rc, gen_out, st_after, run_rc) = _guard_run(
+        tune, wn, L, H, D, V, B, 2, fuse=True, after=_generate_and_rerun)
     assert frc == [llm_capi.LLM_ERR_RANGE] * 2 and fst == (1, 0), (frc, fst)
+    # generate over the clamping model: every step clamps, yet every
+    # id is produced; the status comes back once, at the end
+    assert gen_rc == llm_capi.LLM_ERR_RANGE, gen_rc
+    assert gen_out.min() >= 0 and gen_out.max() < V, gen_out
+    assert st_after == (0, 1, 0), st_after  # sync after generate: reported; status: clamped
+    # a timing re-run of the clamping attention has its own flag: the sync
+    # after it succeeds
+    assert run_rc == (0, 0), run_rc
+
+
+def _generate_and_rerun(lib, dec):
+    """llm_decoder_generate on a clamping decoder (output pre-filled with -1),
+    then sync / oproj_status, then llm_decoder_run_attention(layer 0) + sync."""
+    lib.llm_decoder_generate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_void_p]
+    lib.llm_decoder_run_attention.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    B, n_gen, plen = 3, 4, 2
+    prompts = np.arange(B * plen, dtype=np.int32).reshape(B, plen)
+    lens = np.full(B, plen, np.int32)
+    out = np.full((B, n_gen), -1, np.int32)
+    rc = lib.llm_decoder_generate(dec, prompts.ctypes.data, lens.ctypes.data, plen, B, n_gen,
+                                  ctypes.c_float(1.0), out.ctypes.data)
+    sync_rc = lib.llm_decoder_sync(dec)
+    clamped, nz = ctypes.c_int(-1), ctypes.c_longlong(-1)
+    lib.llm_decoder_oproj_status(dec, ctypes.byref(clamped), ctypes.byref(nz))
+    run = lib.llm_decoder_run_attention(dec, 0, None)
+    return rc, out, (sync_rc, clamped.value, nz.value), (run, lib.llm_decoder_sync(dec))
