@@ -201,6 +201,39 @@ def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
           f"logits rel err {worst:.2e}")
 
 
+@pytest.mark.timeout(900)
+def test_int8_c5_shipped_launch_vs_oracle(gpu, oracle):
+    """C5's exact per-GPU launch (bench.py --config c5 on each of the 8 GPUs):
+    64 rows x 32 heads x D 128 at T 8192, one layer.  The plan is the one the
+    bench runs -- 5 splits of ceil(513 / 5) = 103 pages (derived on device from
+    each row's context), merged over 32 heads and quantised per 4096-wide row
+    by pa_merge_row_kernel -- and the GEMMs are C5's four shapes at 64 rows in
+    the decoder's own packed-A form (qkv 4096x12288, o_proj 4096x4096, fc1
+    4096x16384, fc2 16384x4096).  Every row's pages are read back into the
+    oracle and the step is teacher forced at the four int8 GEMM inputs
+    (attention_cpu/cpu_attention_kernel.cpp:103-120, attention_cpu/int8_quant.cpp:5-13,
+    decoder/mlp.hpp:23-41): each within one LSB, < 1e-3 of the attention values
+    flipped, logits at 1e-3 per row."""
+    from oracle.oracle import OracleDecoder
+    rows, T = 64, 8192
+    w, dec = _int8_decoder(oracle, 1, 32, 128, 512, T + 8, rows, seed=55)
+    c = w["cfg"]
+    assert (c["hid"], c["inter"]) == (4096, 16384)
+    taps = _Taps(dec, c, rows)
+    dec.begin_synthetic(rows, T, 80, True)
+    ns, form = dec.attention_plan()
+    assert (ns, form) == (5, FORM_SPLIT_MERGE_ROW), (ns, form)
+    ntiles = (T + 1 + 15) // 16  # the step attends its own new token too: 513 tiles
+    assert -(-ntiles // ns) == 103, ntiles  # pages per split, as the kernel derives them
+    odec = OracleDecoder(oracle, w, rows)
+    distinct = decoder_kv_to_oracle(dec, odec, rows, T)
+    assert distinct[0] == rows * 32 * (T // 16), distinct  # every (row, head, tile) its own page
+    flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=6)
+    assert flips < 1e-3 * vals, (flips, vals)
+    print(f"C5 shipped launch: {ns} splits (split + merge_row), attention int8 flips "
+          f"{flips}/{vals}, logits rel err {worst:.2e}")
+
+
 def test_int8_c4_beam_state_attention_vs_oracle(gpu, oracle):
     """The C4 bench state (begin_beams(8, 4, 3840, 256): 240 shared tiles per
     sequence through page-table forks, 16 private per beam) at C3 head dims,
