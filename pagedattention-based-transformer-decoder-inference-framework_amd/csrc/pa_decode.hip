@@ -328,7 +328,8 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
       return te;
     }
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
-                                        false, true>), grid, block, 0, st, a);
+                                        false, true, LLM_F16, true, false, false, 0, false, true>),
+                       grid, block, 0, st, a);
     *beam = true;
   } else if (direct) {
     hipLaunchKernelGGL((pa_split_kernel<D, TS, true, 16384, kKvLoadAux, ST>), grid, block, 0, st, a);
@@ -523,7 +524,8 @@ hipError_t beam_occupancy(int* blocks) {
   hipError_t e;
   if (tune_beam_occupancy(D, TS, blocks, &e)) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      blocks, pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true>,
+      blocks, pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true,
+                              LLM_F16, true, false, false, 0, false, true>,
       256, 0);
 }
 

@@ -165,10 +165,16 @@ constexpr int kKvLoadAux = 2;
 // WGM: the workgroup-merge form (PaSplitArgs::wgm): blockDim = 64 * nsplit,
 // one workgroup per (b, h), wave w = split w.
 // OPROJ (WGM only): the fused o_proj of the FP16 decoder (PaSplitArgs::o_acc).
+// INTERLEAVE (BEAM, dynamic splits): split s holds the row's tiles s, s + NS,
+// s + 2 NS, ... instead of a contiguous range.  Every split then holds the
+// same mix of shared-prefix and beam-private tiles (C4: 30 shared + 2 private
+// of 257), so the splits finish together without a cost model, and the split's
+// page ids are requested at entry (their tile indices need no context length)
+// instead of after a 512-tile prefix scan and its barrier.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int RING = 0, bool STAMPS = false>
+          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -183,6 +189,8 @@ void pa_split_kernel(PaSplitArgs a) {
   static_assert(LPT >= 1 && LPT <= 64 && TS % TPI == 0 && NI >= 1, "bad D/TS");
 
   static_assert(!(WGM && (DIRECT || BEAM)), "the workgroup merge is a split form");
+  static_assert(!INTERLEAVE || BEAM, "interleaved splits are a beam-group form");
+  constexpr bool IL = BEAM && INTERLEAVE;
   static_assert(!OPROJ || (WGM && KVT == LLM_F16), "the fused o_proj is a workgroup-merge form");
   const unsigned long long t_entry = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
   const int lane = lane_id();
@@ -206,8 +214,14 @@ void pa_split_kernel(PaSplitArgs a) {
   constexpr int kPfx = 512;
   bool share = false;
   int grow[4] = {0, 0, 0, 0};  // BEAM: the group's page-table rows
-  int idv[BEAM ? kPfx / 64 : 1];
-  const bool pfx_on = BEAM && a.balance16 >= 16 && a.pps == 0 && a.nsplit > 1;
+  int idv[BEAM && !IL ? kPfx / 64 : 1];
+  const bool pfx_on = BEAM && !IL && a.balance16 >= 16 && a.pps == 0 && a.nsplit > 1;
+  // IL: interleaved splits (dynamic split length, groups that share: 4 rows
+  // of equal context; ragged groups keep the plain schedule's contiguous
+  // splits); ilp0 / ilp1 = this wave's row's page ids of tiles s + NS lane and
+  // s + NS (64 + lane), requested before `share` is known
+  bool il = IL && a.pps == 0 && a.nsplit > 1;
+  int ilp0 = -1, ilp1 = -1;
   if constexpr (BEAM) {
     const int g0 = b - gi;
     int Ti[4];
@@ -219,17 +233,24 @@ void pa_split_kernel(PaSplitArgs a) {
     }
     const bool own_ok = grow[gi] >= 0 && grow[gi] < a.num_beams;
     const int32_t* prow = a.page_table + ((size_t)(own_ok ? grow[gi] : 0) * a.H + h) * a.max_tiles;
-    const int lim0 = min(a.max_tiles, kPfx);
+    if constexpr (IL) {
+      const int t0 = s + a.nsplit * lane, t1 = s + a.nsplit * (64 + lane);
+      ilp0 = il && own_ok && t0 < a.max_tiles ? prow[t0] : -1;
+      ilp1 = il && own_ok && t1 < a.max_tiles ? prow[t1] : -1;
+    } else {
+      const int lim0 = min(a.max_tiles, kPfx);
 #pragma unroll
-    for (int k = 0; k < kPfx / 64; ++k) {
-      const int t = 64 * k + lane;
-      idv[k] = pfx_on && own_ok && t < lim0 ? prow[t] : -1;
+      for (int k = 0; k < kPfx / 64; ++k) {
+        const int t = 64 * k + lane;
+        idv[k] = pfx_on && own_ok && t < lim0 ? prow[t] : -1;
+      }
     }
     share = g0 + 3 < a.B;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       share = share && grow[i] >= 0 && grow[i] < a.num_beams &&
               min(max(Ti[i], 0), a.T) == min(max(Ti[0], 0), a.T);
+    il = il && share;
   }
   if (b >= a.B) return;
   const int bh = b * a.H + h;
@@ -239,16 +260,22 @@ void pa_split_kernel(PaSplitArgs a) {
   Tb = min(max(Tb, 0), a.T);
   const int ntiles = min((Tb + TS - 1) / TS, a.max_tiles);
   int tile0, count;
-  {
+  // tiles of the split: tile0 + j * tstride, j < count
+  int tstride = 1;
+  if (IL && il) {
+    tile0 = s;
+    tstride = a.nsplit;
+    count = ntiles > s ? (ntiles - s + a.nsplit - 1) / a.nsplit : 0;
+  } else {
     const int pps = row_pps(a.pps, a.nsplit, ntiles);
     tile0 = s * pps;
     count = min(pps, ntiles - tile0);
   }
   // BEAM: the page ids of the group's 4 rows, tiles [0, pfx_lim), read once
   // by the prefix scan below and reused for this split's page ids
-  __shared__ int pfx_lds[BEAM ? 4 : 1][BEAM ? kPfx : 1];
+  __shared__ int pfx_lds[BEAM && !IL ? 4 : 1][BEAM && !IL ? kPfx : 1];
   int pfx_lim = 0;
-  if constexpr (BEAM) {
+  if constexpr (BEAM && !IL) {
     // Cost-balanced splits: a split's beam-private tiles are loaded by every
     // wave (4x the per-wave bytes of a shared tile, which the workgroup loads
     // once), so equal tile counts leave the splits holding the private tail
@@ -350,7 +377,10 @@ void pa_split_kernel(PaSplitArgs a) {
   // Page ids of this split: lane j holds pages j and 64 + j
   // (PageTable::lookup semantics: out of range or >= num_pages -> missing).
   int pid0 = -1, pid1 = -1;
-  if (BEAM && tile0 + count <= pfx_lim) {  // (r is the group's row gi: read by the prefix scan)
+  if (IL && il) {  // requested at entry (r is the group's row gi)
+    pid0 = lane < count && ilp0 < a.num_pages ? ilp0 : -1;
+    pid1 = 64 + lane < count && ilp1 < a.num_pages ? ilp1 : -1;
+  } else if (BEAM && tile0 + count <= pfx_lim) {  // (r is the group's row gi: read by the prefix scan)
     if (lane < count) pid0 = pfx_lds[gi][tile0 + lane];
     if (64 + lane < count) pid1 = pfx_lds[gi][tile0 + 64 + lane];
   } else if (r >= 0 && r < a.num_beams) {
@@ -451,8 +481,9 @@ void pa_split_kernel(PaSplitArgs a) {
       const int j = p0 + u;
       const int pg = page_of(min(j, kMaxPps - 1));
       const bool ok = (j < count) && (pg >= 0);
-      const int tok_base = (tile0 + j) * TS + g;
-      if (FULLPATH && ok && (tile0 + j + 1) * TS <= Tb)
+      const int tile = tile0 + j * (IL ? tstride : 1);
+      const int tok_base = tile * TS + g;
+      if (FULLPATH && ok && (tile + 1) * TS <= Tb)
         page_math(std::true_type{}, u, ok, tok_base);
       else
         page_math(std::false_type{}, u, ok, tok_base);

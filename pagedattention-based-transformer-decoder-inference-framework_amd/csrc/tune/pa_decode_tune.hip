@@ -768,7 +768,7 @@ hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st
     constexpr int R = decltype(r)::value;
     constexpr bool LO = decltype(lo)::value;
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, LO, true, LLM_F16,
-                                        true, false, false, R>),
+                                        true, false, false, R, false, true>),
                        grid, dim3(256), 0, st, a);
   };
   auto by_ring = [&](auto lo) {
@@ -805,9 +805,14 @@ hipError_t tune_launch_beam_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t
   PaSplitArgs a = a0;
   a.stamps = g_stamps;
   g_stamps_waves = waves;
-  hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
-                                      true, false, false, 0, true>),
-                     grid, dim3(256), 0, st, a);
+  if (env_int("LLM_BEAM_INTERLEAVE", 1) == 0)
+    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
+                                        true, false, false, 0, true>),
+                       grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
+                                        true, false, false, 0, true, true>),
+                       grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -938,6 +943,12 @@ bool tune_launch_form(const PaSplitArgs& a, int D, int TS, dim3 grid, hipStream_
   const int ring = env_int("LLM_BEAM_RING", 0);
   if (ring > 0) {  // shared chunks through an LDS-DMA ring
     *e = tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
+    return true;
+  }
+  if (env_int("LLM_BEAM_INTERLEAVE", 1) == 0) {  // round 4's contiguous cost-balanced splits
+    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true>),
+                       grid, dim3(256), 0, st, a);
+    *e = hipGetLastError();
     return true;
   }
   return false;

@@ -97,7 +97,8 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
     cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1),
     its one-wave-per-group kernel (LLM_BEAM4=1), the shipped form fed by an
-    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits) and the
+    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits), round 4's
+    contiguous cost-balanced splits (LLM_BEAM_INTERLEAVE=0) and the
     dynamic-assignment form (LLM_BEAM_STEAL=1)."""
     import torch
     import llm_capi
@@ -183,6 +184,16 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
                                   lib=llm_capi.load_tune()).cpu().numpy()
         assert np.array_equal(outr.view(np.uint32), outg.view(np.uint32)), (ring, rel_err(outr, outg))
     monkeypatch.delenv("LLM_BEAM_RING")
+    # ... and round 4's contiguous, cost-balanced splits (a 512-tile prefix scan
+    # in every workgroup) in place of the interleaved ones
+    monkeypatch.setenv("LLM_BEAM_INTERLEAVE", "0")
+    outc = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                              beam_ids=d(beam_ids), row_group=4,
+                              lib=llm_capi.load_tune()).cpu().numpy()
+    assert np.isfinite(outc).all()
+    assert_parity(outc, ref, 1e-3)
+    assert rel_err(outc, plain) < 1e-5
+    monkeypatch.delenv("LLM_BEAM_INTERLEAVE")
     # ... and the decoder's form: tiles assigned to the splits while the launch
     # runs (pa_beam_steal.hpp; standalone here on the tuning build's own
     # counters, LLM_BEAM_STEAL=1).  Run three times: the counters must come
