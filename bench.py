@@ -136,24 +136,24 @@ def attention_launch_bytes(cfg, T, B, unique=False):
     return 2 * kv_tokens * H * D * 2 + B * H * nt * 4 + 2 * B * H * D * 4
 
 
-def time_attention(dec, iters=20, row_group=None):
-    """Live HIP-event timing of the decoder's own paged-attention launch of
-    layer 0 (llm_decoder_run_attention: the step graph's kernels, grid and
-    outputs -- split + merge-and-quantise for INT8, the workgroup-merge form
-    for FP16, the beam-group schedule for beams), enqueued on torch's current
-    stream so the events bracket exactly those kernels."""
+def time_attention(dec, layers, iters=24):
+    """Live HIP-event timing of the decoder's own paged-attention launch
+    (llm_decoder_run_attention: the step graph's kernels, grid and outputs --
+    split + merge-and-quantise for INT8, the workgroup-merge form for FP16,
+    the beam-group schedule for beams), enqueued on torch's current stream so
+    the events bracket exactly those kernels.  The launches rotate over the
+    `layers` layers, as in the step: relaunching one layer back to back lets
+    the 256 MiB Infinity Cache re-serve a KV zone that fits it (C2: 101 MB per
+    layer, 21.0 vs 22.3 us; scripts/attn_rotate.py)."""
     import torch
     st = torch.cuda.current_stream().cuda_stream
-
-    def run():
-        dec.run_attention(0, st)
-    for _ in range(3):
-        run()
+    for i in range(3):
+        dec.run_attention(i % layers, st)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        run()
+    for i in range(iters):
+        dec.run_attention(i % layers, st)
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / iters * 1e-3
@@ -555,7 +555,7 @@ def main():
     if dec is not None and rank == 0:
         T_now = dec.context_len(0)
         nsplit, form = dec.attention_plan()
-        t_attn = time_attention(dec)
+        t_attn = time_attention(dec, cfg["L"])
         attn_b = attention_launch_bytes(cfg, T_now, B, unique=True) + fused_weight_bytes(cfg, form)
         achieved = attn_b / t_attn / 1e9
         ratio = load_traffic(args.config)
@@ -574,7 +574,8 @@ def main():
                           + (OPROJ_OUT if form & 32 else FORM_OUT.get(cfg["cls"], {}).get(form & 15, ""))
                           + f", {nsplit} splits, {B} rows (the step's own launch, "
                             "llm_decoder_run_attention)",
-                "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2)}
+                "bytes_per_launch": attn_b, "launch_us": round(t_attn * 1e6, 2),
+                "launch_timing": f"HIP events over 24 launches rotating over the {cfg['L']} layers"}
         if "beams" in cfg:  # logical bytes: every beam reads its whole context
             logical = attention_launch_bytes(cfg, T_now, B)
             roof["bytes_note"] = "achieved counts shared prefix pages once per sequence"

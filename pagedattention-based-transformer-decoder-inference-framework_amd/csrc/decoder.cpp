@@ -31,7 +31,6 @@
 #include "common.hpp"
 #include "gemm.hpp"
 #include "kv_cache_impl.hpp"
-#include "mlp_fused.hpp"
 #include "pa_decode.hpp"
 #include "row_ops.hpp"
 
@@ -143,11 +142,6 @@ struct llm_decoder {
   float top_p = 1.f;
   uint64_t sample_seed = 0;
   bool use_graph = true;  // LLM_GRAPH=0: eager launches (per-kernel profiling)
-  // FP16 decode rows: LN2 -> fc1 -> fc2 as ONE launch (mlp_fused.hip) with
-  // slices of mlp_slice fc1 column tiles per workgroup, when mlp_fusable
-  // (LLM_MLP_FUSE / LLM_MLP_SLICE, read at create)
-  bool mlp_fuse = false;
-  int mlp_slice = 4;
   int qa_ld = 0;
   size_t b16 = 0;  // max_batch rounded up to 16-row tiles
 
@@ -246,8 +240,6 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   // C4 -5 %, C3 -0.5..+1 %: the branches do not overlap usefully, and a
   // saturating KV scan slows the other half's glue 4-8x).
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
-  d->mlp_fuse = env_int("LLM_MLP_FUSE", 0) != 0;
-  d->mlp_slice = env_int("LLM_MLP_SLICE", 4);
   d->h_pos.assign(B, 0);
   *out = d.release();
   return LLM_OK;
@@ -577,32 +569,6 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   if (!R.oacc) RET_IF(weight_gemm(g, st));  // (fused: the attention wrote x)
   g.ln_x = nullptr; g.ln_quant_only = 0; g.act_out = nullptr; g.sa_out = nullptr;
   RET_IF(tap(l, 1, R, hid, st));
-  if (!i8 && mlp_fuse && R.prefill_row < 0 && oacc.p && mlp_fusable(R.n, hid, inter, mlp_slice)) {
-    // LN2 -> fc1 -> fc2 in one launch: fc2's slice partials in the counted
-    // int64 columns (zero here: the fused o_proj completed and cleared them)
-    MlpFusedArgs m{};
-    m.x = R.x;
-    m.ln_g = ln2_g.p + lh;
-    m.ln_b = ln2_b.p + lh;
-    m.eps = 1e-5f;
-    m.w1 = w1.p + sz_1 * l;
-    m.b1 = b1.p + (size_t)l * inter;
-    m.w2 = w2.p + sz_2 * l;
-    m.b2 = b2.p + lh;
-    m.acc = oacc.p + (size_t)R.table_row0 * hid;
-    m.out = R.x;
-    m.flag = oflag.p;
-    m.act_out = tap_q ? static_cast<uint8_t*>(R.act) : nullptr;  // the taps read them back
-    m.h_out = tap_q ? static_cast<_Float16*>(R.act2) : nullptr;
-    m.M = R.n;
-    m.hid = hid;
-    m.inter = inter;
-    m.nslice = inter / (16 * mlp_slice);
-    m.w_keep = w_keep;
-    LLM_HIP_RET(launch_mlp_f16_fused(m, mlp_slice, st));
-    RET_IF(tap(l, 2, R, hid, st));
-    return tap(l, 3, R, inter, st);
-  }
   // LN2 -> mlp_fc1 (+b1, ReLU)
   RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
@@ -789,9 +755,9 @@ int llm_decoder::report_range(int flag) {
   LLM_HIP_RET(hipMemsetAsync(oflag.p, 0, sizeof(int), stream));
   LLM_HIP_RET(hipStreamSynchronize(stream));
   return fail(LLM_ERR_RANGE,
-              "decoder: a term of a fused reduction (an o_proj head product, or an MLP slice's "
-              "fc2 partial) left its fixed-point range (|v| > (2^23 - 1) / terms, or not "
-              "finite) and was clamped; the affected hidden values of that step are wrong");
+              "decoder: a head product of the fused o_proj left its fixed-point range "
+              "(|v| > (2^23 - 1) / num_heads, or not finite) and was clamped; the affected "
+              "hidden values of that step are wrong");
 }
 
 int llm_decoder::oproj_range_status() {

@@ -328,7 +328,7 @@ hipError_t launch_split(const PaSplitArgs& a, bool direct, hipStream_t st, bool*
       return te;
     }
     hipLaunchKernelGGL((pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES,
-                                        false, true, LLM_F16, true, false, false, 0, false, true>),
+                                        false, true, LLM_F16, true, false, false, 0, false, true, true>),
                        grid, block, 0, st, a);
     *beam = true;
   } else if (direct) {
@@ -525,7 +525,7 @@ hipError_t beam_occupancy(int* blocks) {
   if (tune_beam_occupancy(D, TS, blocks, &e)) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(
       blocks, pa_split_kernel<D, TS, false, LLM_BEAM_CHUNK, kKvLoadAux, 2, LLM_BEAM_WAVES, false, true,
-                              LLM_F16, true, false, false, 0, false, true>,
+                              LLM_F16, true, false, false, 0, false, true, true>,
       256, 0);
 }
 

@@ -171,10 +171,17 @@ constexpr int kKvLoadAux = 2;
 // of 257), so the splits finish together without a cost model, and the split's
 // page ids are requested at entry (their tile indices need no context length)
 // instead of after a 512-tile prefix scan and its barrier.
+// PRIO (BEAM): wave priority falls with the shared-chunk progress (3 at entry,
+// 2 / 1 / 0 after a quarter / half / three quarters).  A CU holds 4 beam
+// workgroups dispatched one after another; at equal priority the SIMD arbiter
+// favours the oldest waves, so the first workgroup placed on a CU finishes
+// long before the last (C4 stamps: exits 34 / 39 / 45 / 52 us by dispatch
+// slot), and the last runs alone with 16 KiB in flight.  Priority outranks age
+// (MI355X_MICROARCH.md, two waves per SIMD, item 4): the laggards catch up.
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false>
+          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false, bool PRIO = false>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -193,6 +200,7 @@ void pa_split_kernel(PaSplitArgs a) {
   constexpr bool IL = BEAM && INTERLEAVE;
   static_assert(!OPROJ || (WGM && KVT == LLM_F16), "the fused o_proj is a workgroup-merge form");
   const unsigned long long t_entry = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  if constexpr (BEAM && PRIO) __builtin_amdgcn_s_setprio(3);
   const int lane = lane_id();
   const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
   const int G = BEAM ? 4 : WGM ? 1 : a.group;
@@ -609,6 +617,11 @@ void pa_split_kernel(PaSplitArgs a) {
         if (nsh > 1) quarter(qr, 1);
         __syncthreads();
         for (int cc = 0; cc < nsh; ++cc) {
+          if constexpr (PRIO) {  // (uniform: nsh and cc are)
+            if (cc == nsh / 4) __builtin_amdgcn_s_setprio(2);
+            if (cc == nsh / 2) __builtin_amdgcn_s_setprio(1);
+            if (cc == (3 * nsh) / 4) __builtin_amdgcn_s_setprio(0);
+          }
           const int cur = cc & 1;
           u32x4 kk[NR], vv[NR];
 #pragma unroll

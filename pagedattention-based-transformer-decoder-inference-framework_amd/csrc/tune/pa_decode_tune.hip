@@ -768,7 +768,7 @@ hipError_t tune_launch_beam_ring(const PaSplitArgs& a, dim3 grid, hipStream_t st
     constexpr int R = decltype(r)::value;
     constexpr bool LO = decltype(lo)::value;
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, LO, true, LLM_F16,
-                                        true, false, false, R, false, true>),
+                                        true, false, false, R, false, true, true>),
                        grid, dim3(256), 0, st, a);
   };
   auto by_ring = [&](auto lo) {
@@ -809,9 +809,13 @@ hipError_t tune_launch_beam_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
                                         true, false, false, 0, true>),
                        grid, dim3(256), 0, st, a);
+  else if (env_int("LLM_BEAM_PRIO", 1) == 0)
+    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
+                                        true, false, false, 0, true, true, false>),
+                       grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
-                                        true, false, false, 0, true, true>),
+                                        true, false, false, 0, true, true, true>),
                        grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -943,6 +947,13 @@ bool tune_launch_form(const PaSplitArgs& a, int D, int TS, dim3 grid, hipStream_
   const int ring = env_int("LLM_BEAM_RING", 0);
   if (ring > 0) {  // shared chunks through an LDS-DMA ring
     *e = tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
+    return true;
+  }
+  if (env_int("LLM_BEAM_PRIO", 1) == 0) {  // interleaved splits without the priority ranking
+    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
+                                        true, false, false, 0, false, true, false>),
+                       grid, dim3(256), 0, st, a);
+    *e = hipGetLastError();
     return true;
   }
   if (env_int("LLM_BEAM_INTERLEAVE", 1) == 0) {  // round 4's contiguous cost-balanced splits

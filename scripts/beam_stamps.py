@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=1)
     ap.add_argument("--config", default="c4")
+    ap.add_argument("--tag", default="", help="suffix of the saved .npy")
     args = ap.parse_args()
     import torch
     import bench
@@ -44,7 +45,7 @@ def main():
                                             max_batch=B, page_size=cfg["ts"])
     dec.set_weights(bench.make_weights(cfg, 1234))
     dec.begin_beams(cfg["seqs"], cfg["beams"], cfg["shared"], T - cfg["shared"], 1234, True)
-    us = bench.time_attention(dec, iters=20) * 1e6
+    us = bench.time_attention(dec, cfg["L"], iters=20) * 1e6
     ns, form = dec.attention_plan()
     print(f"{args.config} attention launch (split + merge) {us:.2f} us, {ns} splits, form {form}")
 
@@ -74,6 +75,7 @@ def main():
         raise SystemExit("no stamps recorded (not a beam launch?)")
     s = buf[:n]
     live = s[:, 3] > 0
+    wid = np.nonzero(live)[0]
     s = s[live].astype(np.int64)
     t0 = s[:, 0].min()
     ent, ld, sh, ex = [(s[:, i] - t0) / 100.0 for i in range(4)]  # 100 MHz -> us
@@ -96,7 +98,25 @@ def main():
     print("waves per XCC:", np.bincount(xcc, minlength=8).tolist())
     print("exit p90 per XCC:", [round(float(np.percentile(ex[xcc == x], 90)), 2)
                                 for x in range(8) if np.any(xcc == x)])
-    np.save(os.path.join(ROOT, "gpurun_out", f"beam_stamps_{args.config}.npy"), s)
+    # where the late waves are: by split, head, sequence (the grid's
+    # decomposition: wid = ((seq * H + head) * nsplit + split) * 4 + beam), and
+    # by how many waves their CU held
+    H = cfg["H"]
+    split, rest = (wid // 4) % ns, (wid // 4) // ns
+    head, seq = rest % H, rest // H
+    for name, key, k in (("split", split, ns), ("head", head, H), ("seq", seq, rest.max() + 1)):
+        print(f"exit p50 / p90 by {name}:", " ".join(
+            f"{int(i)}:{np.percentile(ex[key == i], 50):.1f}/{np.percentile(ex[key == i], 90):.1f}"
+            for i in range(int(k)) if np.any(key == i)))
+    cu_id = (xcc << 8) | ((hw >> 8) & 0xFF)  # CU, SH, SE within the XCC
+    _, inv, cnt = np.unique(cu_id, return_inverse=True, return_counts=True)
+    per = cnt[inv]
+    print("waves per CU (count of CUs):", dict(zip(*np.unique(cnt, return_counts=True))))
+    for c in sorted(set(per.tolist())):
+        print(f"  waves whose CU held {c}: exit p50 {np.percentile(ex[per == c], 50):.1f} "
+              f"p90 {np.percentile(ex[per == c], 90):.1f}")
+    np.save(os.path.join(ROOT, "gpurun_out", f"beam_stamps_{args.config}{args.tag}.npy"),
+            np.concatenate([wid[:, None], s], axis=1))
 
 
 def steal_report(lib, args):

@@ -36,7 +36,7 @@ for B in args.rows:
                  stream=torch.cuda.current_stream().cuda_stream, want_next=False)
     torch.cuda.synchronize()
     ns, form = dec.attention_plan()
-    ts = sorted(bench.time_attention(dec, iters=50) for _ in range(5))
+    ts = sorted(bench.time_attention(dec, 1, iters=50) for _ in range(5))
     t = ts[2]
     by = bench.attention_launch_bytes(cfg, dec.context_len(0), B)
     print(f"ctx {dec.context_len(0)} ", end="")

@@ -255,18 +255,13 @@ def test_int8_c4_beam_state_attention_vs_oracle(gpu, oracle):
     print(f"C4 state: {ns} splits, attention int8 flips {flips}/{vals}, logits {worst:.2e}")
 
 
-@pytest.mark.parametrize("mlp", [0, 4], ids=["mlp_gemms", "mlp_fused"])
-def test_f16_step_workgroup_merge_vs_oracle(gpu, oracle, mlp, monkeypatch):
+def test_f16_step_workgroup_merge_vs_oracle(gpu, oracle):
     """C2 dims (12 heads x 64, 16 rows, T 2048): the FP16 decoder's attention
     merges its splits inside the split workgroup (3 splits) and writes the
     packed fp16 o_proj input, compared with the oracle's fp32 attention, and
     adds its o_proj into the fused columns (LLM_PA_FORM_OPROJ).  The tapped
     LN1 rows and the appended K / V are held to the oracle's own within one
-    fp16 ulp, like the GEMM inputs.  mlp_fused: LN2 -> fc1 -> fc2 as the one
-    fused launch (csrc/mlp_fused.hip, 48 slices of 64 inter columns), its LN2
-    and fc1 taps teacher forced like the GEMM forms' (decoder/mlp.hpp:23-41)."""
-    monkeypatch.setenv("LLM_MLP_FUSE", "1" if mlp else "0")
-    monkeypatch.setenv("LLM_MLP_SLICE", str(mlp or 4))
+    fp16 ulp, like the GEMM inputs."""
     torch = _torch()
     import llm_decoder
     from oracle.oracle import OracleDecoder
