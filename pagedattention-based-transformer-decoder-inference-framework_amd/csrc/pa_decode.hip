@@ -639,7 +639,7 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
     const int f = tn.beam_nsplit;
     if (f >= 2 && (long long)f * kMaxPps >= ntiles_max) nsplit = std::min(f, kMaxSplits);
   }
-  if (rows && (rows->out16 || oproj) && !rows->q && row_group == 1 && pps_fixed <= 0) {
+  if (rows && (rows->out16 || oproj || f32_rows) && !rows->q && row_group == 1 && pps_fixed <= 0) {
     const int f = tn.wgm_splits;
     if (f >= 2 && f <= kWgmMaxSplits && (long long)f * kMaxPps >= ntiles_max) nsplit = f;
   }
