@@ -813,6 +813,7 @@ hipError_t tune_launch_beam_stamps(const PaSplitArgs& a0, dim3 grid, hipStream_t
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
                                         true, false, false, 0, true, true, false>),
                        grid, dim3(256), 0, st, a);
+
   else
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
                                         true, false, false, 0, true, true, true>),
