@@ -210,6 +210,9 @@ def fused_weight_bytes(cfg, form):
     return 2 * hid * hid if form & 32 else 0
 
 
+TORCHRUN_CPU_SHARE = 16  # the GPU pool's OpenMP share of a 1-GPU job
+
+
 def cpu_threads():
     """Threads of the CPU baseline: the job's OpenMP share (OMP_NUM_THREADS:
     the GPU pool gives each 1-GPU job 16 of the host's CPUs and sets it so;
@@ -220,6 +223,11 @@ def cpu_threads():
     except AttributeError:
         avail = os.cpu_count() or 1
     env = os.environ.get("OMP_NUM_THREADS", "")
+    if env == "1" and "TORCHELASTIC_RUN_ID" in os.environ:
+        # torch.distributed.run sets OMP_NUM_THREADS=1 in every worker it
+        # starts; the baseline keeps the 1-GPU job's share instead, so it is
+        # the same measurement at every N
+        env = str(TORCHRUN_CPU_SHARE)
     n = int(env) if env.isdigit() and int(env) > 0 else avail
     return min(n, avail), avail
 
@@ -243,6 +251,11 @@ def cpu_baseline(cfg_name, budget_s=20.0):
     res["cpu"]["cpus_available"] = avail  # (the child's own affinity is one place once bound)
     res["omp"] = {"OMP_NUM_THREADS": threads, "OMP_PROC_BIND": "close", "OMP_PLACES": "cores"}
     env_omp = os.environ.get("OMP_NUM_THREADS", "")
+    if env_omp == "1" and "TORCHELASTIC_RUN_ID" in os.environ:
+        res["threads_reason"] = (
+            f"torch.distributed.run set OMP_NUM_THREADS=1 in this worker; the baseline keeps a "
+            f"1-GPU job's OpenMP share ({threads} of {avail} CPUs in the affinity mask)")
+        return res
     res["threads_reason"] = (
         f"the job's OpenMP share: OMP_NUM_THREADS={env_omp} set by the GPU pool for a 1-GPU job "
         f"on a host shared by 8 GPUs' jobs ({avail} CPUs in the affinity mask); BASELINE.md asks "

@@ -87,3 +87,26 @@ def test_rank_count_must_equal_gpus():
                env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=60)
     assert r.returncode != 0
     assert "--gpus 2 but the launcher started 1 rank" in r.stderr
+
+
+def test_torchrun_launch_and_cpu_baseline_share():
+    """The driver's multi-GPU form: torch.distributed.run starts the ranks
+    (WORLD_SIZE set, no self-spawn) and sets OMP_NUM_THREADS=1 in each; the
+    CPU baseline on rank 0 keeps the 1-GPU job's OpenMP share."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in LAUNCH_ENV + ("OMP_NUM_THREADS",)}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), str(ROOT / "bench.py"), "--gpus", "2", "--config", "c1",
+                        "--stub-step", "--steps", "2", "--warmup", "1", "--cpu-budget", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    res = _line(r)
+    assert res["n_gpus"] == 2 and res["process_group"]["size"] == 2
+    cpu = res["cpu_baseline"]
+    avail = len(os.sched_getaffinity(0))
+    assert cpu["cores"] == min(16, avail), cpu
+    assert "torch.distributed.run" in cpu["threads_reason"]
