@@ -8,65 +8,6 @@
 
 namespace llm {
 
-// sum_s part[s * stride] * w_s over s < ns with w_s held by lane s (s < 64) /
-// lane s - 64 of w1: loads issued 8 splits at a time so a merge costs a few
-// memory round trips, not one per split; summation order s = 0, 1, ...
-__device__ __forceinline__ float merge_splits(const float* part, int stride, int ns, float w0,
-                                              float w1) {
-  float acc = 0.f;
-  for (int s0 = 0; s0 < ns; s0 += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = (s0 + u < ns) ? part[(size_t)(s0 + u) * stride] : 0.f;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int s2 = s0 + u;
-      if (s2 < ns) {
-        const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
-        acc += v[u] * ws;
-      }
-    }
-  }
-  return acc;
-}
-
-// Split merge (flash-decoding LSE combine): one wave per (b, h).
-struct PaMergeArgs {
-  const float* part_acc;
-  const float* part_ml;
-  float* out;
-  const int32_t* context_lens;
-  int B, H, D, T, TS, pps, nsplit, max_tiles;
-};
-
-__global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
-  const int lane = lane_id();
-  const int bh = blockIdx.x * 4 + wave_id_uniform();
-  if (bh >= a.B * a.H) return;
-  const int b = bh / a.H;
-  int Tb = a.context_lens ? a.context_lens[b] : a.T;
-  Tb = min(max(Tb, 0), a.T);
-  const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
-  const int pps = row_pps(a.pps, a.nsplit, ntiles);
-  // pps < 0: every split holds a partial (beam launches: cost-balanced splits)
-  const int ns = a.pps < 0 ? a.nsplit : min(a.nsplit, (ntiles + pps - 1) / pps);
-  const float* ml = a.part_ml + (size_t)bh * a.nsplit * 2;
-  float M = kNegSentinel;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, ml[2 * s]);
-  float* o = a.out + (size_t)bh * a.D;
-  if (ns <= 0 || M <= 0.5f * kNegSentinel) {
-    for (int d = lane; d < a.D; d += 64) o[d] = 0.f;
-    return;
-  }
-  float L = 0.f;
-  for (int s = 0; s < ns; ++s) L += ml[2 * s + 1] * __builtin_amdgcn_exp2f(ml[2 * s] - M);
-  const float inv = 1.0f / (L + 1e-6f);
-  const float* pa = a.part_acc + (size_t)bh * a.nsplit * a.D;
-  const float w0 = lane < ns ? __builtin_amdgcn_exp2f(ml[2 * lane] - M) : 0.f;
-  const float w1 = 64 + lane < ns ? __builtin_amdgcn_exp2f(ml[2 * (64 + lane)] - M) : 0.f;
-  for (int d = lane; d < a.D; d += 64) o[d] = merge_splits(pa + d, a.D, ns, w0, w1) * inv;
-}
-
 // Split merge fused with the next consumer's input conversion: one workgroup
 // per row b merges all H heads into an LDS row [H*D], then writes any of
 //   out   fp32 [B][H*D]            (pa_decode's output)
@@ -86,10 +27,120 @@ struct PaMergeRowArgs {
   int ctx_p0;  // >= 0 and context_lens NULL: row b's context is ctx_p0 + b + 1 (prefill)
 };
 
-// DPL = output dims per lane (D / 64, at least 1).  A head's split weights
-// (m, l) and the partials of its first kMergeBatch splits are loaded together,
-// so a merge costs one memory round trip (splits beyond the batch: one more
-// per batch); summation order s = 0, 1, ... as pa_merge_kernel.
+// One head's split merge (flash-decoding LSE combine) by one wave, DPL =
+// output dims per lane (D / 64, at least 1).  The head's split weights (m, l),
+// lane-parallel (lane holds splits lane and 64 + lane), and the partials of
+// its first BATCH splits are loaded together: every address depends on the
+// launch's arguments only (clamped to its nsplit), so they issue with the
+// caller's context_lens load and a merge costs one memory round trip (splits
+// beyond the batch: one more per 8).  The row's split count ns masks the
+// values afterwards (splits past ns may hold stale bits).  Summation order
+// s = 0, 1, ... (sequential) for L and for every output; split s's (l, w) come
+// from lane s by readlane.  acc[j] * the returned 1 / L is the output at dim
+// lane + 64 j; a head with no partial returns acc = 0.
+template <int DPL, int BATCH>
+__device__ __forceinline__ float merge_head(const float* ml, const float* pa, int nsplit, int ns,
+                                            int D, float (&acc)[DPL]) {
+  const int lane = lane_id();
+  const int nsl = max(nsplit - 1, 0);
+  const float m0r = ml[2 * min(lane, nsl)], l0r = ml[2 * min(lane, nsl) + 1];
+  const float m1r = ml[2 * min(64 + lane, nsl)], l1r = ml[2 * min(64 + lane, nsl) + 1];
+  float v[BATCH][DPL];
+#pragma unroll
+  for (int s2 = 0; s2 < BATCH; ++s2)
+#pragma unroll
+    for (int j = 0; j < DPL; ++j)
+      v[s2][j] = pa[(size_t)min(s2, nsl) * D + min(lane + 64 * j, D - 1)];
+  const float m0 = lane < ns ? m0r : kNegSentinel;
+  const float m1 = 64 + lane < ns ? m1r : kNegSentinel;
+  const float l0 = lane < ns ? l0r : 0.f;
+  const float l1 = 64 + lane < ns ? l1r : 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < BATCH; ++s2)
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) v[s2][j] = s2 < ns ? v[s2][j] : 0.f;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+  const float M = ln_wave_max(fmaxf(m0, m1));
+  if (ns <= 0 || M <= 0.5f * kNegSentinel) return 0.f;
+  const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
+  const float w1 = 64 + lane < ns ? __builtin_amdgcn_exp2f(m1 - M) : 0.f;
+  float L = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < BATCH; ++s2)
+    if (s2 < ns) {
+      const float ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l0), s2));
+      const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
+      L += ls * ws;
+    }
+  for (int s2 = BATCH; s2 < ns; ++s2) {
+    const float ls = s2 < 64 ? __shfl(l0, s2, 64) : __shfl(l1, s2 - 64, 64);
+    const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
+    L += ls * ws;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < BATCH; ++s2) {
+    const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));  // 0 past ns
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] += v[s2][j] * ws;
+  }
+  for (int s0 = BATCH; s0 < ns; s0 += 8) {  // long split lists
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) {
+      const int d = lane + 64 * j;
+      float u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = (s0 + k < ns && d < D) ? pa[(size_t)(s0 + k) * D + d] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int s2 = s0 + k;
+        if (s2 < ns) {
+          const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
+          acc[j] += u[k] * ws;
+        }
+      }
+    }
+  }
+  return 1.0f / (L + 1e-6f);
+}
+
+// Split merge, fp32 output: one wave per (b, h), 4 per workgroup.  The first
+// 16 splits' partials come in the first round trip (the 8-row C3 step merges
+// 16 splits per head: 8.0 us per launch when the (m, l) and partial loads
+// were issued split by split).
+struct PaMergeArgs {
+  const float* part_acc;
+  const float* part_ml;
+  float* out;
+  const int32_t* context_lens;
+  int B, H, D, T, TS, pps, nsplit, max_tiles;
+};
+
+template <int DPL>
+__global__ __launch_bounds__(256) void pa_merge_kernel(PaMergeArgs a) {
+  const int lane = lane_id();
+  const int bh = blockIdx.x * 4 + wave_id_uniform();
+  if (bh >= a.B * a.H) return;
+  const int b = bh / a.H;
+  int Tb = a.context_lens ? a.context_lens[b] : a.T;
+  Tb = min(max(Tb, 0), a.T);
+  const int ntiles = min((Tb + a.TS - 1) / a.TS, a.max_tiles);
+  const int pps = row_pps(a.pps, a.nsplit, ntiles);
+  // pps < 0: every split holds a partial (beam launches: cost-balanced splits)
+  const int ns = a.pps < 0 ? a.nsplit : min(a.nsplit, (ntiles + pps - 1) / pps);
+  float acc[DPL];
+  const float inv = merge_head<DPL, 16>(a.part_ml + (size_t)bh * a.nsplit * 2,
+                                        a.part_acc + (size_t)bh * a.nsplit * a.D, a.nsplit, ns,
+                                        a.D, acc);
+  float* o = a.out + (size_t)bh * a.D;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) {
+    const int d = lane + 64 * j;
+    if (d < a.D) o[d] = acc[j] * inv;
+  }
+}
+
+// Splits per first round trip of pa_merge_row_kernel's heads.
 constexpr int kMergeBatch = 8;
 
 template <int DPL>
@@ -109,83 +160,11 @@ __global__ __launch_bounds__(1024) void pa_merge_row_kernel(PaMergeRowArgs a) {
   const int ns = a.pps < 0 ? a.nsplit : min(a.nsplit, (ntiles + pps - 1) / pps);
   for (int h = w; h < a.H; h += nw) {
     const size_t bh = (size_t)b * a.H + h;
-    const float* ml = a.part_ml + bh * a.nsplit * 2;
-    const float* pa = a.part_acc + bh * a.nsplit * a.D;
-    // split weights, lane-parallel: lane holds splits lane and 64 + lane.
-    // Every load's address depends on kernel arguments only (clamped to the
-    // launch's nsplit), so they issue together with the context_lens load
-    // instead of after it (one round trip, not two); the row's split count
-    // ns masks the values afterwards (splits past ns may hold stale bits).
-    const int nsl = max(a.nsplit - 1, 0);
-    const float m0r = ml[2 * min(lane, nsl)], l0r = ml[2 * min(lane, nsl) + 1];
-    const float m1r = ml[2 * min(64 + lane, nsl)], l1r = ml[2 * min(64 + lane, nsl) + 1];
-    float v[kMergeBatch][DPL];
-#pragma unroll
-    for (int s2 = 0; s2 < kMergeBatch; ++s2)
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) {
-        const int d = lane + 64 * j;
-        v[s2][j] = pa[(size_t)min(s2, nsl) * a.D + min(d, a.D - 1)];
-      }
-    const float m0 = lane < ns ? m0r : kNegSentinel;
-    const float m1 = 64 + lane < ns ? m1r : kNegSentinel;
-    const float l0 = lane < ns ? l0r : 0.f;
-    const float l1 = 64 + lane < ns ? l1r : 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < kMergeBatch; ++s2)
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) v[s2][j] = s2 < ns ? v[s2][j] : 0.f;
-    const float M = ln_wave_max(fmaxf(m0, m1));
-    float* dst = row + h * a.D;
-    if (ns <= 0 || M <= 0.5f * kNegSentinel) {
-      for (int d = lane; d < a.D; d += 64) dst[d] = 0.f;
-      continue;
-    }
-    const float w0 = lane < ns ? __builtin_amdgcn_exp2f(m0 - M) : 0.f;
-    const float w1 = 64 + lane < ns ? __builtin_amdgcn_exp2f(m1 - M) : 0.f;
-    // same summation order as pa_merge_kernel: s = 0, 1, ... (sequential);
-    // split s's (l, w) come from lane s by readlane (SALU broadcast, no LDS
-    // round trip per split), the first kMergeBatch unrolled
-    float L = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < kMergeBatch; ++s2)
-      if (s2 < ns) {
-        const float ls = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l0), s2));
-        const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));
-        L += ls * ws;
-      }
-    for (int s2 = kMergeBatch; s2 < ns; ++s2) {
-      const float ls = s2 < 64 ? __shfl(l0, s2, 64) : __shfl(l1, s2 - 64, 64);
-      const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
-      L += ls * ws;
-    }
-    const float inv = 1.0f / (L + 1e-6f);
     float acc[DPL];
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int s2 = 0; s2 < kMergeBatch; ++s2) {
-      const float ws = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w0), s2));  // 0 past ns
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) acc[j] += v[s2][j] * ws;
-    }
-    for (int s0 = kMergeBatch; s0 < ns; s0 += 8) {  // long splits lists (rare)
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) {
-        const int d = lane + 64 * j;
-        float u[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) u[k] = (s0 + k < ns && d < a.D) ? pa[(size_t)(s0 + k) * a.D + d] : 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int s2 = s0 + k;
-          if (s2 < ns) {
-            const float ws = s2 < 64 ? __shfl(w0, s2, 64) : __shfl(w1, s2 - 64, 64);
-            acc[j] += u[k] * ws;
-          }
-        }
-      }
-    }
+    const float inv = merge_head<DPL, kMergeBatch>(a.part_ml + bh * a.nsplit * 2,
+                                                   a.part_acc + bh * a.nsplit * a.D, a.nsplit, ns,
+                                                   a.D, acc);
+    float* dst = row + h * a.D;
 #pragma unroll
     for (int j = 0; j < DPL; ++j) {
       const int d = lane + 64 * j;
@@ -493,7 +472,13 @@ int llm::pa_merge_splits_internal(const float* part_acc, const float* part_ml, f
                                   const int32_t* context_lens, int B, int H, int D, int T, int TS,
                                   int pps, int nsplit, int max_tiles, hipStream_t st) {
   PaMergeArgs mg{part_acc, part_ml, out, context_lens, B, H, D, T, TS, pps, nsplit, max_tiles};
-  hipLaunchKernelGGL(pa_merge_kernel, dim3((B * H + 3) / 4), dim3(256), 0, st, mg);
+  const dim3 grid((B * H + 3) / 4);
+  if (D <= 64)
+    hipLaunchKernelGGL(pa_merge_kernel<1>, grid, dim3(256), 0, st, mg);
+  else if (D <= 128)
+    hipLaunchKernelGGL(pa_merge_kernel<2>, grid, dim3(256), 0, st, mg);
+  else
+    hipLaunchKernelGGL(pa_merge_kernel<4>, grid, dim3(256), 0, st, mg);
   LLM_HIP_RET(hipGetLastError());
   return LLM_OK;
 }
