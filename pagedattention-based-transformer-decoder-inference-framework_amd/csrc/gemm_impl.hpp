@@ -602,7 +602,12 @@ namespace {
 
 // Column tiles per workgroup: 2 when that still leaves >= 192 workgroups
 // (measured: qkv 9.9 vs 12.2 us, fc1 10.5 vs 12.5 us at M = 64), else 1.
+// At <= 16 rows A is one 16-row fragment per k-step, so sharing it over two
+// column tiles saves little and halves the workgroups streaming the weights:
+// 1 (C3 shapes at M = 8, graph-replayed, profiles/r05/gemm_small_m.txt: qkv
+// 5.28 -> 4.95 us, fc1 5.96 -> 5.25 us).
 inline int pick_nt(int N, int M) {
+  if (M <= 16) return 1;
   const int ntiles = (N + 15) / 16;
   const int mblocks = (M + 63) / 64;
   return (ntiles % 2 == 0 && (ntiles / 2) * mblocks >= 192) ? 2 : 1;
