@@ -181,9 +181,8 @@ constexpr int kKvLoadAux = 2;
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false, bool PRIO = false,
-          int QUADS = 1>
-__global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256 * QUADS)
+          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false, bool PRIO = false>
+__global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
   constexpr int ES = kv_elem_bytes<KVT>();
@@ -203,12 +202,7 @@ void pa_split_kernel(PaSplitArgs a) {
   const unsigned long long t_entry = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if constexpr (BEAM && PRIO) __builtin_amdgcn_s_setprio(3);
   const int lane = lane_id();
-  static_assert(QUADS == 1 || (BEAM && INTERLEAVE && RING == 0 && !STAMPS),
-                "several beam groups per workgroup: the interleaved LDS-staged form only");
-  const int wid = blockIdx.x * (WGM ? a.nsplit : 4 * QUADS) + wave_id_uniform();
-  // QUADS > 1 (tuning build): the workgroup holds QUADS beam groups' splits
-  // (4 waves each, wave w in group w / 4) which meet at every barrier
-  const int sub = QUADS > 1 ? wave_id_uniform() >> 2 : 0;
+  const int wid = blockIdx.x * (WGM ? a.nsplit : 4) + wave_id_uniform();
   const int G = BEAM ? 4 : WGM ? 1 : a.group;
   const int gi = wid % G;  // row within the group (fastest: adjacent waves)
   const int rest = wid / G;
@@ -515,10 +509,8 @@ void pa_split_kernel(PaSplitArgs a) {
     static_assert(NR % 2 == 0, "beam prefetch splits a chunk's 2*NR pieces in quarters");
     constexpr int QP = NR / 2;  // pieces per wave per chunk
     static_assert(RING == 0 || (RING >= 3 && (RING - 2) * QP < 64), "ring of 3+ chunks");
-    __shared__ int pid_lds_all[QUADS][4][128];
-    __shared__ __attribute__((aligned(16))) u32x4 kvbuf_all[QUADS][RING > 0 ? RING : 2][2 * NR][64];
-    auto& pid_lds = pid_lds_all[sub];
-    auto& kvbuf = kvbuf_all[sub];
+    __shared__ int pid_lds[4][128];
+    __shared__ __attribute__((aligned(16))) u32x4 kvbuf[RING > 0 ? RING : 2][2 * NR][64];
     if (share) {
       pid_lds[gi][lane] = pid0;
       pid_lds[gi][64 + lane] = pid1;

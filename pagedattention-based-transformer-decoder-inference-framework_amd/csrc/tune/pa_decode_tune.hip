@@ -950,24 +950,6 @@ bool tune_launch_form(const PaSplitArgs& a, int D, int TS, dim3 grid, hipStream_
     *e = tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
     return true;
   }
-  if (env_int("LLM_BEAM_QUADS", 0) == 4 && grid.x % 4 == 0) {
-    // 4 beam groups' splits per 16-wave workgroup (one workgroup per CU at
-    // C4), meeting at every shared-chunk barrier: lockstep progress instead
-    // of the SIMD arbiter's oldest-first order between 4 separate workgroups.
-    // Needs every group of a workgroup to run the same barrier sequence (all
-    // share, equal shared-chunk counts: the uniform C4 bench state) --
-    // experiment only.
-    if (env_int("LLM_BEAM_PRIO", 1) == 0)
-      hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
-                                          true, false, false, 0, false, true, false, 4>),
-                         dim3(grid.x / 4), dim3(1024), 0, st, a);
-    else
-      hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
-                                          true, false, false, 0, false, true, true, 4>),
-                         dim3(grid.x / 4), dim3(1024), 0, st, a);
-    *e = hipGetLastError();
-    return true;
-  }
   if (env_int("LLM_BEAM_PRIO", 1) == 0) {  // interleaved splits without the priority ranking
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
                                         true, false, false, 0, false, true, false>),
