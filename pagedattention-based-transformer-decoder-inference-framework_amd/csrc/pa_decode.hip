@@ -606,9 +606,20 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   // leave 2 of the 8 slots idle): C3 6 -> 8 splits
   const bool f32_rows = rows && rows->f32_rows && !rows->q && !rows->out16;
   const PaTuning tn = pa_tuning();
-  const bool wgm_ok = ((row_out && rows->out16 && !rows->q) || oproj || f32_rows) && row_group == 1 &&
-                      kv->kv_dtype == LLM_F16 && tn.wg_merge;
   int nsplit = choose_nsplit(B, H, ntiles_max, pps_fixed, resident_launch);
+  // fp32 rows whose launch is exactly one resident round of more splits than
+  // a workgroup merge holds (C3's model at 8 rows per GPU: 128 (row, head)
+  // pairs x 16 splits of 33 pages = 2,048 waves): half the splits, twice as
+  // long, still split + merge.  Standalone (scripts/tune_attention.py --B 8,
+  // profiles/r05/attention_b8_split_sweep.txt): 85.6 -> 84.3 us, the
+  // loads-only form 83.7 / 83.4 us at either count.
+  const bool half_round = f32_rows && row_group == 1 && pps_fixed <= 0 &&
+                          kv->kv_dtype == LLM_F16 && nsplit > kWgmMaxSplits &&
+                          (long long)B * H * nsplit == resident_launch &&
+                          (ntiles_max + nsplit - 1) / nsplit <= 2 * kShortPps;
+  if (half_round) nsplit = (nsplit + 1) / 2;
+  const bool wgm_ok = ((row_out && rows->out16 && !rows->q) || oproj || f32_rows) && row_group == 1 &&
+                      kv->kv_dtype == LLM_F16 && tn.wg_merge && !half_round;
   if (wgm_ok && pps_fixed <= 0 && !f32_rows) {
     const int nw = choose_nsplit(B, H, ntiles_max, 0, resident_launch, kWgmShortPps);
     if (nw >= 2 && nw <= kWgmMaxSplits) nsplit = nw;
