@@ -292,6 +292,19 @@ int kv_cache_remove(kv_cache* c, int layer, int beam, int head, int tile);
 /* KVTileCache::register_tile (kv_tile_cache.cpp:64-77): allocate a free page
  * for (layer, beam, head, tile) if it has none; returns the page id in *page. */
 int kv_cache_register_tile(kv_cache* c, int layer, int beam, int head, int tile, int* page);
+/* Page-pool exhaustion policy of kv_cache_register_tile.  LLM_EVICT_NONE (the
+ * default): LLM_ERR_OOM.  LLM_EVICT_LRU: KVTileCache's policy
+ * (kv_cache/kv_tile_cache.cpp:64-98, update_lru / evict_if_needed): every
+ * register_tile call makes its tile the most recently used, and a tile that
+ * needs a page when none is free takes one by removing the least recently
+ * registered tile whose page that frees (an entry on a page a forked beam
+ * still shares is kept) -- the reference's semantics, so an evicted tile of a
+ * live sequence reads as missing (masked) afterwards.  Only tiles registered
+ * through kv_cache_register_tile are candidates; the decoder's own pages
+ * (reserve / append) never are.  Switching the policy keeps the recency list. */
+#define LLM_EVICT_NONE 0
+#define LLM_EVICT_LRU 1
+int kv_cache_set_eviction(kv_cache* c, int policy);
 /* Ensure pages exist for tiles covering tokens [0, n_tokens) of `beam`, all layers/heads. */
 int kv_cache_reserve(kv_cache* c, int beam, int n_tokens);
 /* Beam fork: dst's page-table rows := src's (all layers, heads), shared pages

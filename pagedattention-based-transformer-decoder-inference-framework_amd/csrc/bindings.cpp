@@ -310,6 +310,14 @@ class KVTileCache {
     need();
     return kv_cache_lookup(c_, layer, beam, head, tile);
   }
+  // "lru": KVTileCache's eviction when the pool is full (kv_tile_cache.cpp:89-98);
+  // "none" (default): register_tile raises instead
+  void set_eviction(const std::string& policy) {
+    need();
+    if (policy != "lru" && policy != "none")
+      throw std::invalid_argument("KVTileCache.set_eviction: policy must be 'lru' or 'none'");
+    check(kv_cache_set_eviction(c_, policy == "lru" ? LLM_EVICT_LRU : LLM_EVICT_NONE));
+  }
   void fork(int src, int dst) { need(); check(kv_cache_fork(c_, src, dst)); }
   void release(int beam) { need(); check(kv_cache_release(c_, beam)); }
   void sync_page_table_to_gpu() { need(); check(kv_cache_sync(c_, nullptr)); check(llm_sync()); }
@@ -479,6 +487,7 @@ PYBIND11_MODULE(llm_decoder, m) {
            py::arg("tile_id"), py::arg("layer") = 0)
       .def("lookup", &KVTileCache::lookup, py::arg("beam_id"), py::arg("head_id"),
            py::arg("tile_id"), py::arg("layer") = 0)
+      .def("set_eviction", &KVTileCache::set_eviction, py::arg("policy"))
       .def("fork", &KVTileCache::fork)
       .def("release", &KVTileCache::release)
       .def("sync_page_table_to_gpu", &KVTileCache::sync_page_table_to_gpu)

@@ -176,6 +176,34 @@ int KvCache::ensure_tile(int layer, int beam, int head, int tile, bool exclusive
   return LLM_OK;
 }
 
+void KvCache::lru_touch(size_t idx) {  // KVTileCache::update_lru, kv_tile_cache.cpp:79-87
+  auto it = lru_pos.find(idx);
+  if (it != lru_pos.end()) lru.erase(it->second);
+  lru.push_front(idx);
+  lru_pos[idx] = lru.begin();
+}
+
+// KVTileCache::evict_if_needed (kv_tile_cache.cpp:89-98): remove the least
+// recently registered entry whose page that frees.  Entries another call has
+// already removed are dropped from the list; entries on a page a forked beam
+// still shares stay (evicting them would free nothing, and the reference has
+// no shared pages), so a pool held only by shared pages still reports OOM.
+bool KvCache::lru_evict_one() {
+  for (auto it = lru.end(); it != lru.begin();) {
+    --it;
+    const size_t idx = *it;
+    const int32_t p = h_table[idx];
+    if (p >= 0 && refcount[p] > 1) continue;
+    lru_pos.erase(idx);
+    it = lru.erase(it);
+    if (p < 0) continue;
+    drop_page(p);
+    set_entry(idx, -1);
+    return true;
+  }
+  return false;
+}
+
 int KvCache::prepare_append(int beam, int pos) {
   const int tile = pos / TS;
   if (tile >= max_tiles)
@@ -331,10 +359,27 @@ extern "C" int kv_cache_register_tile(kv_cache* c, int layer, int beam, int head
   KvCache& k = c->impl;
   std::lock_guard<std::mutex> g(k.mu);
   LLM_REQUIRE(k.in_range(layer, beam, head, tile), "kv_cache_register_tile: index out of range");
+  const size_t idx = k.index(layer, beam, head, tile);
   int32_t p;
   int rc = k.ensure_tile(layer, beam, head, tile, false, &p);
+  // LRU policy: a tile without a page takes one by evicting the least recently
+  // registered entries (an entry sharing a forked page frees nothing, so the
+  // next one goes too) until a page is free or nothing is left to evict
+  while (rc == LLM_ERR_OOM && k.evict == LLM_EVICT_LRU && k.lru_evict_one())
+    rc = k.ensure_tile(layer, beam, head, tile, false, &p);
   if (rc) return rc;
+  k.lru_touch(idx);  // (under either policy, so switching to LRU later sees the order)
   if (page) *page = p;
+  return LLM_OK;
+}
+
+extern "C" int kv_cache_set_eviction(kv_cache* c, int policy) {
+  LLM_REQUIRE(c, "kv_cache_set_eviction: NULL");
+  LLM_REQUIRE(policy == LLM_EVICT_NONE || policy == LLM_EVICT_LRU,
+              "kv_cache_set_eviction: policy must be LLM_EVICT_NONE or LLM_EVICT_LRU");
+  KvCache& k = c->impl;
+  std::lock_guard<std::mutex> g(k.mu);
+  k.evict = policy;
   return LLM_OK;
 }
 
@@ -402,6 +447,8 @@ extern "C" int kv_cache_clear(kv_cache* c) {
   k.cow.clear();
   std::fill(k.refcount.begin(), k.refcount.end(), 0);
   k.reset_free_lists();
+  k.lru.clear();
+  k.lru_pos.clear();
   LLM_HIP_RET(hipMemset(k.d_table, 0xFF, k.entries * sizeof(int32_t)));
   LLM_HIP_RET(hipDeviceSynchronize());  // null-stream memset vs. non-blocking user streams
   return LLM_OK;

@@ -5,7 +5,9 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <list>
 #include <mutex>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -42,6 +44,15 @@ struct KvCache {
   size_t staging_cap = 0;
   hipEvent_t staging_done = nullptr;
   std::mutex mu;
+  // kv_cache_set_eviction: LLM_EVICT_LRU makes register_tile evict the least
+  // recently registered table entries when the pool is exhausted
+  // (kv_tile_cache.cpp:79-98).  lru: table indices, most recent first; entries
+  // removed by other calls stay in it until an eviction skips them.
+  int evict = LLM_EVICT_NONE;
+  std::list<size_t> lru;
+  std::unordered_map<size_t, std::list<size_t>::iterator> lru_pos;
+  void lru_touch(size_t idx);
+  bool lru_evict_one();  // false: nothing left to evict
 
   ~KvCache();
   int init(int L, int beams, int H, int D, int TS, int max_tiles, long long pages,

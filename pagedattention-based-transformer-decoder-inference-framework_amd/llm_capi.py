@@ -23,6 +23,7 @@ TUNE_LIB_PATH = HERE / "libllm_decoder_hip_tune.so"  # `make tune`: A/B hooks, n
  LLM_ERR_RANGE) = range(7)
 LLM_F16, LLM_I8, LLM_F32, LLM_BF16 = 0, 1, 2, 3
 LLM_ACT_NONE, LLM_ACT_RELU, LLM_ACT_GELU = 0, 1, 2
+LLM_EVICT_NONE, LLM_EVICT_LRU = 0, 1
 
 c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 c_ll = ctypes.c_longlong
@@ -99,6 +100,7 @@ _SIGS = {
     "kv_cache_lookup": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
     "kv_cache_remove": (c_int, [c_void_p, c_int, c_int, c_int, c_int]),
     "kv_cache_register_tile": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_i32p]),
+    "kv_cache_set_eviction": (c_int, [c_void_p, c_int]),
     "kv_cache_reserve": (c_int, [c_void_p, c_int, c_int]),
     "kv_cache_fork": (c_int, [c_void_p, c_int, c_int]),
     "kv_cache_release": (c_int, [c_void_p, c_int]),

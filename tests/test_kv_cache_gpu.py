@@ -70,6 +70,98 @@ def test_kv_cache_alloc_fork_cow(gpu):
         lib.kv_cache_destroy(h)
 
 
+class _RefLru:
+    """KVTileCache<T>::register_tile / update_lru / evict_if_needed
+    (kv_cache/kv_tile_cache.cpp:64-98) restated over tile keys: which tiles
+    hold a page, and the recency order (most recent first).  The reference's
+    page ids (map.size(), kv_tile_cache.cpp:71) alias live pages after an
+    eviction, so page ids are not compared -- only which tiles are mapped."""
+
+    def __init__(self, total):
+        self.total, self.mapped, self.lru = total, set(), []
+
+    def register(self, key):
+        if key not in self.mapped:
+            if len(self.mapped) >= self.total:  # evict_if_needed
+                self.mapped.discard(self.lru.pop())
+            self.mapped.add(key)
+        if key in self.lru:  # update_lru
+            self.lru.remove(key)
+        self.lru.insert(0, key)
+
+
+def test_kv_cache_lru_eviction_vs_reference(gpu):
+    """kv_cache_set_eviction(LLM_EVICT_LRU): a random stream of register_tile
+    calls over more tiles than the pool holds keeps exactly the reference's
+    set of mapped tiles after every call, on distinct pages; the default
+    policy reports LLM_ERR_OOM and changes nothing; kv_cache_clear resets the
+    recency list; the pybind KVTileCache.set_eviction drives the same path."""
+    import llm_capi
+    lib = llm_capi.load()
+    pages = 6
+    h = ctypes.c_void_p()
+    llm_capi.check(lib.kv_cache_create(2, 2, 2, 64, 16, 8, pages, ctypes.byref(h)))
+    try:
+        keys = [(l, b, hh, t) for l in range(2) for b in range(2) for hh in range(2) for t in range(8)]
+        page = ctypes.c_int32()
+        for k in keys[:pages]:
+            llm_capi.check(lib.kv_cache_register_tile(h, *k, ctypes.byref(page)))
+        # default policy: the pool is full -> OOM, no entry touched
+        before = [lib.kv_cache_lookup(h, *k) for k in keys]
+        assert lib.kv_cache_register_tile(h, *keys[pages], ctypes.byref(page)) == llm_capi.LLM_ERR_OOM
+        assert [lib.kv_cache_lookup(h, *k) for k in keys] == before
+        llm_capi.check(lib.kv_cache_clear(h))
+        llm_capi.check(lib.kv_cache_set_eviction(h, llm_capi.LLM_EVICT_LRU))
+        assert lib.kv_cache_set_eviction(h, 7) == llm_capi.LLM_ERR_INVALID
+        ref = _RefLru(pages)
+        rng = np.random.default_rng(3)
+        pool = keys[:10]  # 10 tiles competing for 6 pages: hits and evictions
+        for i in range(300):
+            k = pool[int(rng.integers(len(pool)))]
+            llm_capi.check(lib.kv_cache_register_tile(h, *k, ctypes.byref(page)))
+            ref.register(k)
+            got = {kk: lib.kv_cache_lookup(h, *kk) for kk in pool}
+            mapped = {kk for kk, p in got.items() if p >= 0}
+            assert mapped == ref.mapped, (i, k, sorted(mapped ^ ref.mapped))
+            assert got[k] == page.value and 0 <= page.value < pages
+            assert len({got[kk] for kk in mapped}) == len(mapped)  # distinct pages
+            assert lib.kv_cache_free_pages(h) == pages - len(mapped)
+        # a page a forked beam shares is never evicted for nothing: beam 1 of
+        # layer 0 shares beam 0's pages, so only unshared entries can go
+        llm_capi.check(lib.kv_cache_clear(h))
+        for t in range(3):
+            llm_capi.check(lib.kv_cache_register_tile(h, 0, 0, 0, t, ctypes.byref(page)))
+        llm_capi.check(lib.kv_cache_fork(h, 0, 1))  # beam 1 := beam 0 (both layers)
+        for t in range(3, 6):
+            llm_capi.check(lib.kv_cache_register_tile(h, 1, 0, 0, t, ctypes.byref(page)))
+        # pool full (3 shared + 3 own); the LRU entries 0..2 are shared: the
+        # next tile evicts layer 1's tile 3, the oldest unshared one
+        llm_capi.check(lib.kv_cache_register_tile(h, 1, 0, 1, 0, ctypes.byref(page)))
+        assert lib.kv_cache_lookup(h, 1, 0, 0, 3) == -1
+        assert all(lib.kv_cache_lookup(h, 0, 0, 0, t) >= 0 for t in range(3))
+        assert all(lib.kv_cache_lookup(h, 0, 1, 0, t) == lib.kv_cache_lookup(h, 0, 0, 0, t)
+                   for t in range(3))
+        # releasing beam 1 leaves layer 0's tiles 0..2 unshared again, so the
+        # next eviction takes tile 0, now the oldest evictable entry
+        llm_capi.check(lib.kv_cache_release(h, 1))
+        llm_capi.check(lib.kv_cache_register_tile(h, 1, 1, 1, 1, ctypes.byref(page)))
+        assert lib.kv_cache_lookup(h, 0, 0, 0, 0) == -1  # now the oldest, unshared
+    finally:
+        lib.kv_cache_destroy(h)
+    # the pybind KVTileCache (kv_tile_cache.hpp:9-41 names)
+    import llm_decoder
+    c = llm_decoder.KVTileCache()
+    c.init(3, 16, 64, 1, 1, 1, 8, "float16")
+    with pytest.raises(RuntimeError):
+        for t in range(4):
+            c.register_tile(0, 0, t, 0)
+    c.set_eviction("lru")
+    p3 = c.register_tile(0, 0, 3, 0)  # evicts tile 0, the least recently registered
+    assert c.lookup(0, 0, 0, 0) == -1 and p3 >= 0
+    with pytest.raises(ValueError):
+        c.set_eviction("fifo")
+
+
 def test_forked_beams_attention_and_save_load(gpu, oracle, tmp_path):
     """Beams forked from a shared prefix, then diverging tokens written with
     COW; pa_decode over the cache (beam_ids routing) matches the oracle on the
