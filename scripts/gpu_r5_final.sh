@@ -20,3 +20,13 @@ for c in ${CONFIGS:-c3 c4 c2 c1 c5}; do
     || { tail -20 gpurun_out/r05_bench_$c.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/r05_bench_$c.json'));print('$c',d['value'],d['ms_per_step'],d['roofline']['frac'],d['cpu_baseline']['value'])"
 done
+# the N-rank strong path with the real decoder: C3's 64 rows over 2 and 4
+# gloo ranks sharing this one GPU (bench.py starts the ranks itself; the
+# timing is not a scaling number, the ranks share one device)
+if [ -n "$GLOO_REHEARSAL" ]; then
+  for n in 2 4; do
+    LLM_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus $n --steps 5 --warmup 2 --no-cpu-baseline --no-weak-extra > gpurun_out/r05_bench_c3_gloo$n.json 2> gpurun_out/r05_bench_c3_gloo$n.err \
+      || { tail -20 gpurun_out/r05_bench_c3_gloo$n.err; exit 1; }
+    python -c "import json;d=json.load(open('gpurun_out/r05_bench_c3_gloo$n.json'));print('c3 gloo', d['n_gpus'], d['scaling'], d['config']['batch_per_gpu'], d['per_rank_ms_per_step'], d['process_group'], d['gather'])"
+  done
+fi
