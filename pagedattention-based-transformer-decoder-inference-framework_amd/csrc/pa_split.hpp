@@ -181,8 +181,7 @@ constexpr int kKvLoadAux = 2;
 template <int D, int TS, bool DIRECT, int CHUNK_BYTES = 16384, int AUX = kKvLoadAux,
           int STAGES = 2, int MIN_WAVES = 0, bool LOAD_ONLY = false, bool BEAM = false,
           int KVT = LLM_F16, bool FULLPATH = true, bool WGM = false, bool OPROJ = false,
-          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false, bool PRIO = false,
-          bool PRIVFIRST = false>
+          int RING = 0, bool STAMPS = false, bool INTERLEAVE = false, bool PRIO = false>
 __global__ __launch_bounds__(WGM ? 64 * kWgmMaxSplits : 256)
 __attribute__((amdgpu_waves_per_eu(MIN_WAVES > 0 ? MIN_WAVES : 1)))
 void pa_split_kernel(PaSplitArgs a) {
@@ -501,28 +500,6 @@ void pa_split_kernel(PaSplitArgs a) {
 
   const int nchunks = (count + U - 1) / U;
   int ch0 = 0;  // first chunk of the per-wave direct path
-  // PRIVFIRST's per-wave direct path over chunks [c0, c1) (the same loop as
-  // the one after the shared path below, which stays written out: as a
-  // lambda call it changes the product kernels' code)
-  auto direct = [&](int c0, int c1) {
-    if constexpr (STAGES == 1) {
-      u32x4 kA[NR], vA[NR];
-      for (int ch = c0; ch < c1; ++ch) {
-        issue(kA, vA, ch * U);
-        compute(kA, vA, ch * U);
-      }
-    } else if (c0 < c1) {
-      u32x4 kA[NR], vA[NR], kB[NR], vB[NR];
-      issue(kA, vA, c0 * U);
-      for (int ch = c0; ch < c1; ch += 2) {
-        issue(kB, vB, (ch + 1) * U);
-        compute(kA, vA, ch * U);
-        if (ch + 1 >= c1) break;
-        issue(kA, vA, (ch + 2) * U);
-        compute(kB, vB, (ch + 1) * U);
-      }
-    }
-  };
   unsigned long long t_load = 0, t_shared = 0;
   if constexpr (STAMPS) {
     (void)page_of(0);  // the page ids have arrived
@@ -555,9 +532,6 @@ void pa_split_kernel(PaSplitArgs a) {
         if (!all) break;
       }
       nsh = __builtin_amdgcn_readfirstlane(nsh);
-      // PRIVFIRST (tuning build): the beam-private chunks first, the shared
-      // ones (LDS-staged, balanced over the 4 waves) at the end of the launch
-      if constexpr (PRIVFIRST) direct(nsh, nchunks);
       // this wave's quarter of chunk cc: pieces q = gi*QP + t of [K pieces | V pieces]
       auto quarter = [&](u32x4 (&qr)[QP], int cc) {
 #pragma unroll
@@ -665,7 +639,7 @@ void pa_split_kernel(PaSplitArgs a) {
           __syncthreads();
         }
       }
-      ch0 = PRIVFIRST ? nchunks : nsh;
+      ch0 = nsh;
     }
   }
   if constexpr (STAMPS) t_shared = __builtin_amdgcn_s_memrealtime();

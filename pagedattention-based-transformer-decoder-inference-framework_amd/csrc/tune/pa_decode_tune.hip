@@ -950,13 +950,6 @@ bool tune_launch_form(const PaSplitArgs& a, int D, int TS, dim3 grid, hipStream_
     *e = tune_launch_beam_ring(a, grid, st, ring, env_int("LLM_BEAM_DIAG", 0) == 2);
     return true;
   }
-  if (env_int("LLM_BEAM_PRIVFIRST", 0) == 1) {  // the beam-private chunks before the shared ones
-    hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
-                                        true, false, false, 0, false, true, true, true>),
-                       grid, dim3(256), 0, st, a);
-    *e = hipGetLastError();
-    return true;
-  }
   if (env_int("LLM_BEAM_PRIO", 1) == 0) {  // interleaved splits without the priority ranking
     hipLaunchKernelGGL((pa_split_kernel<128, 16, false, 8192, kKvLoadAux, 2, 0, false, true, LLM_F16,
                                         true, false, false, 0, false, true, false>),
