@@ -359,6 +359,21 @@ def spawn_ranks(n, argv):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    import signal
+
+    def stop(signum, _frame):  # the launcher itself stopped (driver timeout, ^C): take the ranks along
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        t_end = time.time() + 10
+        for q in procs:
+            try:
+                q.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+        sys.exit(128 + signum)
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
     rc, deadline = 0, None
     live = dict(enumerate(procs))
     while live:

@@ -110,3 +110,33 @@ def test_torchrun_launch_and_cpu_baseline_share():
     avail = len(os.sched_getaffinity(0))
     assert cpu["cores"] == min(16, avail), cpu
     assert "torch.distributed.run" in cpu["threads_reason"]
+
+
+def test_launcher_sigterm_stops_its_ranks():
+    """The launcher stopped from outside (the driver's timeout, ^C) takes its
+    ranks along instead of leaving them running (a rank blocked in a
+    collective would never exit on its own)."""
+    import signal
+    import time
+
+    import psutil
+    env = {k: v for k, v in os.environ.items() if k not in LAUNCH_ENV}
+    p = subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--stub-step",
+                          "--no-cpu-baseline", "--steps", "1000000", "--warmup", "1"], cwd=ROOT,
+                         env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        kids = []
+        for _ in range(100):
+            kids = psutil.Process(p.pid).children()
+            if len(kids) == 2:
+                break
+            time.sleep(0.1)
+        assert len(kids) == 2, kids
+        time.sleep(2)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 128 + signal.SIGTERM
+        _, alive = psutil.wait_procs(kids, timeout=15)
+        assert not alive, alive
+    finally:
+        if p.poll() is None:
+            p.kill()
