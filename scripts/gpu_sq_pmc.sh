@@ -15,7 +15,7 @@ if [ "${MFMA:-0}" = 1 ]; then
 fi
 cd /tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/sq1 -o sq1 -- python3 $R/scripts/ab_attention_lib.py > /dev/null || exit 1
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace --output-format csv -d $O/sq2 -o sq2 -- python3 $R/scripts/ab_attention_lib.py > /dev/null || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-trace --output-format csv -d $O/sq2 -o sq2 -- python3 $R/scripts/ab_attention_lib.py > /dev/null || exit 1
 python3 - $O <<'PY'
 import csv, glob, json, sys, collections
 O = sys.argv[1]
@@ -39,6 +39,8 @@ for n, cs in vals.items():
     k["frac_wait_any"] = round(k.get("SQ_WAIT_ANY", 0) / wc, 3)
     k["frac_issue_stall"] = round(k.get("SQ_WAIT_INST_ANY", 0) / wc, 3)
     k["frac_valu_active"] = round(k.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3)
+    if k.get("SQ_LDS_IDX_ACTIVE"):
+        k["lds_bank_conflict_per_active"] = round(k.get("SQ_LDS_BANK_CONFLICT", 0) / k["SQ_LDS_IDX_ACTIVE"], 3)
     out["kernels"][n[:80]] = k
 json.dump(out, open(f"{O}/sq_pmc_summary.json", "w"), indent=1)
 for n, k in out["kernels"].items():
