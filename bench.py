@@ -196,7 +196,8 @@ FORM_NAMES = {0: "direct (one split)", 1: "split + pa_merge_kernel",
 # its prologue; the FP16 one reads packed fp16 rows)
 FORM_OUT = {"INT8Decoder": {0: " (fp32 rows; the o_proj prologue quantises them)",
                             1: " (fp32 rows; the o_proj prologue quantises them)",
-                            3: " (fp32 rows; the o_proj prologue quantises them)"},
+                            3: " (fp32 rows; the o_proj prologue quantises them, or a quantise "
+                               "launch for rows wider than 2048)"},
             "CUDADecoder": {3: " (packed fp16 o_proj input)"}}
 # form bit 32: the FP16 decoder's o_proj runs inside the workgroup merge
 OPROJ_OUT = " (o_proj fused: each (row, head) workgroup adds o_h W_o[h] into int64 rows)"

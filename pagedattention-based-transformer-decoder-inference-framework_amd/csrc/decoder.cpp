@@ -149,6 +149,7 @@ struct llm_decoder {
   int layer_attn(int l, hipStream_t st, const struct Rows& R, PaPlan* plan = nullptr);
   bool quant_prologue(const struct Rows& R) const;
   bool oproj_fusable(const struct Rows& R);
+  bool wgm_quant_ok(const struct Rows& R);
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -396,6 +397,10 @@ struct Rows {
   const int32_t* beam_rows = nullptr;  // page-table row per row; NULL: table_row0 + m
   int table_row0 = 0;
   int row_group = 1;
+  // INT8 rows too wide for the o_proj quantising prologue (wgm_quant_ok): the
+  // attention writes fp32 rows merged in the workgroup and a quantise launch
+  // follows it
+  bool wgm_quant = false;
   // prefill chunk (row >= 0): the n rows are positions p0 .. p0+n-1 of page-table
   // row prefill_row, attended causally by the MFMA prefill kernel
   int prefill_row = -1;
@@ -501,6 +506,23 @@ bool llm_decoder::oproj_fusable(const Rows& R) {
   return (p.form & LLM_PA_FORM_OPROJ) != 0;
 }
 
+// INT8 decode rows whose o_proj cannot quantise its own input (hidden >
+// 2048: C5's 4096, 256 KB of fp32 rows per 16-row workgroup): when the plan
+// with fp32 rows is the workgroup merge (<= 8 splits), the attention merges
+// its splits in the workgroup and one quantise launch writes the packed int8
+// o_proj input -- in place of split + pa_merge_row_kernel (C5: 5 splits of
+// 103 pages -> 8 of 65 merged in the workgroup).
+bool llm_decoder::wgm_quant_ok(const Rows& R) {
+  if (wdtype != LLM_I8 || R.prefill_row >= 0 || R.row_group != 1 || R.beam_rows ||
+      quant_prologue(R))
+    return false;
+  Rows r = R;
+  r.wgm_quant = true;
+  PaPlan p;
+  if (layer_attn(0, stream, r, &p) != LLM_OK) return false;
+  return (p.form & 15) == LLM_PA_FORM_WG_MERGE;
+}
+
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
   pa_kv_view view;
   RET_IF(kv_cache_view(kv, l, &view));
@@ -526,8 +548,8 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
   PaRowOutputs ro;
   ro.pack = 1;
   ro.keep_out = 0;
-  if (quant_prologue(R)) {
-    ro.f32_rows = 1;  // fp32 rows in R.o, quantised by the o_proj prologue
+  if (quant_prologue(R) || R.wgm_quant) {
+    ro.f32_rows = 1;  // fp32 rows in R.o, quantised by the o_proj prologue or the launch below
   } else if (wdtype == LLM_I8) {
     ro.q = static_cast<int8_t*>(R.act);
     ro.inv_scale = R.sa;
@@ -542,9 +564,12 @@ int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) 
     ro.out16 = R.act;
   }
   if (R.row_group >= 4 && beam_steal_on()) ro.beam_ctr = beam_ctr.p;
-  return pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
+  RET_IF(pa_decode_internal(&view, R.q, hid, R.o, R.beam_rows, R.ctx, R.n, H, D, cfg.max_seq_len,
                             cfg.attn_scale, pps, R.attn_ws, R.attn_ws_bytes, st, &ro,
-                            R.row_group, plan);
+                            R.row_group, plan));
+  if (R.wgm_quant && !plan)  // the packed int8 o_proj input + row scales
+    LLM_HIP_RET(launch_quantize_rows(R.o, R.n, hid, static_cast<int8_t*>(R.act), R.sa, st, 1));
+  return LLM_OK;
 }
 
 int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
@@ -680,6 +705,7 @@ int llm_decoder::step_tail(hipStream_t st, int r0, int n) {
 int llm_decoder::enqueue_step(hipStream_t st) {
   Rows R = step_rows(0, batch, attn_ws.p);
   if (oproj_fusable(R)) R.oacc = oacc.p, R.oproj_out = R.x, R.oflag = oflag.p;
+  R.wgm_quant = wgm_quant_ok(R);
   RET_IF(step_head(st, 0, batch));
   for (int l = 0; l < L; ++l) {
     RET_IF(layer_pre(l, st, R));
@@ -972,6 +998,7 @@ extern "C" int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form
   LLM_REQUIRE(d->batch > 0, "llm_decoder_attention_plan: no active rows");
   Rows R = d->step_rows(0, d->batch, d->attn_ws.p);
   if (d->oproj_fusable(R)) R.oacc = d->oacc.p, R.oproj_out = R.x, R.oflag = d->oflag.p;
+  R.wgm_quant = d->wgm_quant_ok(R);
   PaPlan p;
   RET_IF(d->layer_attn(0, d->stream, R, &p));
   *nsplit = p.nsplit;
@@ -999,6 +1026,7 @@ extern "C" int llm_decoder_run_attention(llm_decoder* d, int layer, void* stream
     }
     R.oacc = d->oacc_run.p, R.oproj_out = R.o, R.oflag = d->oflag_run.p;
   }
+  R.wgm_quant = d->wgm_quant_ok(R);
   return d->layer_attn(layer, st, R);
 }
 

@@ -180,10 +180,10 @@ def test_int8_c3_shipped_launch_vs_oracle(gpu, oracle):
 @pytest.mark.timeout(600)
 def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
     """C5's per-GPU model dims: 32 heads x D 128 (hid 4096, inter 16384), 2
-    layers, 16 rows at T 2048.  hid 4096 keeps the split + pa_merge_row_kernel
-    form (the o_proj quantising prologue takes K <= 2048 only): the merge
-    launch quantises each 4096-wide row into the o_proj's packed int8 A, and
-    the GEMMs run C5's shapes (qkv 4096x12288, o_proj 4096x4096, fc1
+    layers, 16 rows at T 2048.  hid 4096 is too wide for the o_proj
+    quantising prologue (K <= 2048), so the attention merges its splits in
+    the workgroup into fp32 rows and a quantise launch writes each 4096-wide
+    row into the o_proj's packed int8 A, and the GEMMs run C5's shapes (qkv 4096x12288, o_proj 4096x4096, fc1
     4096x16384, fc2 16384x4096: 256 k-steps) -- against the oracle, teacher
     forced at the four int8 GEMM inputs (attention_cpu/cpu_attention_kernel.cpp:103-120,
     attention_cpu/int8_quant.cpp:5-13, decoder/mlp.hpp:23-41)."""
@@ -194,12 +194,12 @@ def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
     taps = _Taps(dec, w["cfg"], rows)
     dec.begin_synthetic(rows, T, 79, True)
     ns, form = dec.attention_plan()
-    assert form == FORM_SPLIT_MERGE_ROW and ns >= 2, (ns, form)
+    assert form == FORM_WG_MERGE and ns >= 2, (ns, form)
     odec = OracleDecoder(oracle, w, rows)
     decoder_kv_to_oracle(dec, odec, rows, T)
     flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=5)
     assert flips < 1e-3 * vals, (flips, vals)
-    print(f"C5 dims: {ns} splits (split + merge_row), attention int8 flips {flips}/{vals}, "
+    print(f"C5 dims: {ns} splits (workgroup merge + quantise), attention int8 flips {flips}/{vals}, "
           f"logits rel err {worst:.2e}")
 
 
@@ -207,9 +207,9 @@ def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
 def test_int8_c5_shipped_launch_vs_oracle(gpu, oracle):
     """C5's exact per-GPU launch (bench.py --config c5 on each of the 8 GPUs):
     64 rows x 32 heads x D 128 at T 8192, one layer.  The plan is the one the
-    bench runs -- 5 splits of ceil(513 / 5) = 103 pages (derived on device from
-    each row's context), merged over 32 heads and quantised per 4096-wide row
-    by pa_merge_row_kernel -- and the GEMMs are C5's four shapes at 64 rows in
+    bench runs -- 8 splits of ceil(513 / 8) = 65 pages (derived on device from
+    each row's context) merged in the workgroup into fp32 rows, then one
+    launch quantising each 4096-wide row -- and the GEMMs are C5's four shapes at 64 rows in
     the decoder's own packed-A form (qkv 4096x12288, o_proj 4096x4096, fc1
     4096x16384, fc2 16384x4096).  Every row's pages are read back into the
     oracle and the step is teacher forced at the four int8 GEMM inputs
@@ -224,15 +224,15 @@ def test_int8_c5_shipped_launch_vs_oracle(gpu, oracle):
     taps = _Taps(dec, c, rows)
     dec.begin_synthetic(rows, T, 80, True)
     ns, form = dec.attention_plan()
-    assert (ns, form) == (5, FORM_SPLIT_MERGE_ROW), (ns, form)
+    assert (ns, form) == (8, FORM_WG_MERGE), (ns, form)
     ntiles = (T + 1 + 15) // 16  # the step attends its own new token too: 513 tiles
-    assert -(-ntiles // ns) == 103, ntiles  # pages per split, as the kernel derives them
+    assert -(-ntiles // ns) == 65, ntiles  # pages per split, as the kernel derives them
     odec = OracleDecoder(oracle, w, rows)
     distinct = decoder_kv_to_oracle(dec, odec, rows, T)
     assert distinct[0] == rows * 32 * (T // 16), distinct  # every (row, head, tile) its own page
     flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=6)
     assert flips < 1e-3 * vals, (flips, vals)
-    print(f"C5 shipped launch: {ns} splits (split + merge_row), attention int8 flips "
+    print(f"C5 shipped launch: {ns} splits (workgroup merge + quantise), attention int8 flips "
           f"{flips}/{vals}, logits rel err {worst:.2e}")
 
 
