@@ -493,8 +493,10 @@ int llm_decoder_set_taps(llm_decoder* d, int8_t* q_dev, float* s_dev);
  * launch, whose split lengths follow each row's live context).  INT8 decoders
  * whose o_proj quantises its own input (decode rows <= 64, hidden <= 2048, no
  * beam groups) report the fp32-row forms (LLM_PA_FORM_WG_MERGE up to 8
- * splits, else LLM_PA_FORM_SPLIT_MERGE, LLM_PA_FORM_DIRECT); beam groups and
- * wider models LLM_PA_FORM_SPLIT_MERGE_ROW (| LLM_PA_FORM_BEAM).  FP16
+ * splits, else LLM_PA_FORM_SPLIT_MERGE, LLM_PA_FORM_DIRECT); wider models
+ * LLM_PA_FORM_WG_MERGE when their fp32-row plan is one (a quantise launch
+ * follows it), else LLM_PA_FORM_SPLIT_MERGE_ROW; beam groups
+ * LLM_PA_FORM_SPLIT_MERGE_ROW | LLM_PA_FORM_BEAM.  FP16
  * decoders whose launch merges in the workgroup (2..8 splits, head_dim <= 128,
  * <= 64 heads) run o_proj inside it: LLM_PA_FORM_WG_MERGE | LLM_PA_FORM_OPROJ. */
 int llm_decoder_attention_plan(llm_decoder* d, int* nsplit, int* form);
