@@ -12,7 +12,7 @@ for B in 8 16 32; do
   timeout -k 10 300 python bench.py --global-batch $B --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_c3_rows$B.json 2> $O/bench_c3_rows$B.err || { tail -5 $O/bench_c3_rows$B.err; exit 1; }
   python -c "import json;d=json.load(open('$O/bench_c3_rows$B.json'));print('rows $B', d['value'], d['ms_per_step'], d['roofline']['launch_us'])"
 done
-for c in c3 c4 c2 c3b8; do
+for c in c3 c4 c2 c5 c3b8; do
   if [ $c = c3b8 ]; then args="--config c3 --global-batch 8"; else args="--config $c"; fi
   bash scripts/trace_step.sh r05f_$c $args || { echo "trace $c failed"; tail -5 gpurun_out/trace_r05f_$c/bench.err; exit 1; }
   f=$(find gpurun_out/trace_r05f_$c -name "*kernel_trace.csv" | head -1)

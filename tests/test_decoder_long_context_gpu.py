@@ -178,29 +178,32 @@ def test_int8_c3_shipped_launch_vs_oracle(gpu, oracle):
 
 
 @pytest.mark.timeout(600)
-def test_int8_c5_dims_step_vs_oracle(gpu, oracle):
+@pytest.mark.parametrize("rows,T,form", [(16, 2048, FORM_WG_MERGE), (2, 8192, FORM_SPLIT_MERGE_ROW)])
+def test_int8_c5_dims_step_vs_oracle(gpu, oracle, rows, T, form):
     """C5's per-GPU model dims: 32 heads x D 128 (hid 4096, inter 16384), 2
-    layers, 16 rows at T 2048.  hid 4096 is too wide for the o_proj
-    quantising prologue (K <= 2048), so the attention merges its splits in
-    the workgroup into fp32 rows and a quantise launch writes each 4096-wide
-    row into the o_proj's packed int8 A, and the GEMMs run C5's shapes (qkv 4096x12288, o_proj 4096x4096, fc1
-    4096x16384, fc2 16384x4096: 256 k-steps) -- against the oracle, teacher
-    forced at the four int8 GEMM inputs (attention_cpu/cpu_attention_kernel.cpp:103-120,
+    layers.  hid 4096 is too wide for the o_proj quantising prologue (K <=
+    2048), so at 16 rows x T 2048 the attention merges its splits in the
+    workgroup into fp32 rows and a quantise launch writes each 4096-wide row
+    into the o_proj's packed int8 A; at 2 rows x T 8192 the fp32-row plan
+    needs more than 8 splits, so the launch falls back to split +
+    pa_merge_row_kernel (merge and quantise in one launch).  The GEMMs run
+    C5's shapes (qkv 4096x12288, o_proj 4096x4096, fc1 4096x16384, fc2
+    16384x4096: 256 k-steps) -- against the oracle, teacher forced at the four
+    int8 GEMM inputs (attention_cpu/cpu_attention_kernel.cpp:103-120,
     attention_cpu/int8_quant.cpp:5-13, decoder/mlp.hpp:23-41)."""
     from oracle.oracle import OracleDecoder
-    rows, T = 16, 2048
     w, dec = _int8_decoder(oracle, 2, 32, 128, 512, T + 8, rows, seed=54)
     assert w["cfg"]["hid"] == 4096 and w["cfg"]["inter"] == 16384
     taps = _Taps(dec, w["cfg"], rows)
     dec.begin_synthetic(rows, T, 79, True)
-    ns, form = dec.attention_plan()
-    assert form == FORM_WG_MERGE and ns >= 2, (ns, form)
+    ns, got = dec.attention_plan()
+    assert got == form and ns >= 2, (ns, got)
     odec = OracleDecoder(oracle, w, rows)
     decoder_kv_to_oracle(dec, odec, rows, T)
     flips, vals, worst = _forced_steps_int8(dec, odec, taps, rows, T, 2, 512, seed=5)
     assert flips < 1e-3 * vals, (flips, vals)
-    print(f"C5 dims: {ns} splits (workgroup merge + quantise), attention int8 flips {flips}/{vals}, "
-          f"logits rel err {worst:.2e}")
+    print(f"C5 dims, {rows} rows x T {T}: {ns} splits (form {got}), attention int8 flips "
+          f"{flips}/{vals}, logits rel err {worst:.2e}")
 
 
 @pytest.mark.timeout(900)
