@@ -124,7 +124,7 @@ struct llm_decoder {
   float* tap_s = nullptr;
   int tap(int l, int stage, const struct Rows& R, int K, hipStream_t st);
   int layer_norm_into(WeightGemm& g, const struct Rows& R, const float* gamma, const float* beta,
-                      hipStream_t st);
+                      hipStream_t st, float* zero_x = nullptr);
   LnSource embed_src;  // set by step_head: the next LayerNorm reads E[token] rows
 
   ~llm_decoder() {
@@ -150,6 +150,7 @@ struct llm_decoder {
   bool quant_prologue(const struct Rows& R) const;
   bool oproj_fusable(const struct Rows& R);
   bool wgm_quant_ok(const struct Rows& R);
+  bool fc2_split(const struct Rows& R) const;
   int layer_post(int l, hipStream_t st, const struct Rows& R);
   struct Rows step_rows(int r0, int n, uint8_t* ws);
   int step_head(hipStream_t st, int r0, int n);
@@ -457,17 +458,18 @@ int llm_decoder::layer_pre(int l, hipStream_t st, const Rows& R) {
 // the rows' A image fits in LDS (decode rows), else a LayerNorm (+ quant)
 // launch writing the packed A the GEMM reads.
 int llm_decoder::layer_norm_into(WeightGemm& g, const Rows& R, const float* gamma,
-                                 const float* beta, hipStream_t st) {
+                                 const float* beta, hipStream_t st, float* zero_x) {
   // the step's first LayerNorm reads the token embedding rows (step_head)
-  const LnSource src = embed_src;
+  LnSource src = embed_src;
   embed_src = LnSource{};
+  src.zero_x = zero_x;  // (the LayerNorm launch only: the caller checks fc2_split)
   if (R.prefill_row < 0 && ln_fusable(wdtype, R.n, hid)) {
     g.ln_x = R.x; g.ln_g = gamma; g.ln_b = beta; g.ln_eps = 1e-5f;
     g.ln_emb = src.emb; g.ln_tok = src.tok; g.ln_V = src.V;
     if (tap_q) { g.act_out = R.act; g.sa_out = R.sa; }  // the taps read A and the scales back
     return LLM_OK;
   }
-  const LnSource* pp = src.emb ? &src : nullptr;
+  const LnSource* pp = src.emb || src.zero_x ? &src : nullptr;
   if (wdtype == LLM_I8)
     LLM_HIP_RET(launch_layernorm_quant(R.x, R.n, hid, gamma, beta, 1e-5f, nullptr,
                                        static_cast<int8_t*>(R.act), R.sa, st, 1, pp));
@@ -521,6 +523,19 @@ bool llm_decoder::wgm_quant_ok(const Rows& R) {
   PaPlan p;
   if (layer_attn(0, stream, r, &p) != LLM_OK) return false;
   return (p.form & 15) == LLM_PA_FORM_WG_MERGE;
+}
+
+// INT8 decode rows <= 16 (the 4- and 8-GPU points of C3's strong curve): fc2's
+// 128 column tiles leave half the CUs idle, so it runs as two k slices that
+// each add their dequantised half into x (fp32 atomics; two addends commute,
+// so x is the same bits whichever lands first).  x must be zero when fc2
+// starts: the LN2 launch, the last reader of the o_proj output in x, writes
+// zeros over the rows after loading them.  Standalone (scripts/tune_gemm_sk.py,
+// profiles/r05/gemm_small_m.txt): fc2 at M = 8 6.86 -> 5.67 us, M = 16 7.53 ->
+// 5.95 us.
+bool llm_decoder::fc2_split(const Rows& R) const {
+  return wdtype == LLM_I8 && R.prefill_row < 0 && R.n <= 16 && !ln_fusable(wdtype, R.n, hid) &&
+         inter / 64 >= 16;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {
@@ -595,7 +610,8 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.ln_x = nullptr; g.ln_quant_only = 0; g.act_out = nullptr; g.sa_out = nullptr;
   RET_IF(tap(l, 1, R, hid, st));
   // LN2 -> mlp_fc1 (+b1, ReLU)
-  RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st));
+  const bool split_fc2 = fc2_split(R);
+  RET_IF(layer_norm_into(g, R, ln2_g.p + lh, ln2_b.p + lh, st, split_fc2 ? R.x : nullptr));
   g.W_packed = w1.p + sz_1 * l; g.N = inter; g.K = hid;
   g.bias = b1.p + (size_t)l * inter; g.act = LLM_ACT_RELU;
   if (i8) {
@@ -619,6 +635,7 @@ int llm_decoder::layer_post(int l, hipStream_t st, const Rows& R) {
   g.W_packed = w2.p + sz_2 * l; g.N = hid; g.K = inter; g.C = R.x;
   g.bias = b2.p + lh; g.act = LLM_ACT_NONE;
   if (i8) g.sw = sw2.p + lh;
+  g.ksplit2 = split_fc2 ? 1 : 0;  // (x was zeroed by the LN2 launch)
   return weight_gemm(g, st);
 }
 

@@ -137,6 +137,11 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.act_out = static_cast<uint8_t*>(g.act_out);
   a.sa_out = g.sa_out;
   a.w_keep = g.w_keep;
+  LLM_REQUIRE(!g.ksplit2 || (g.dtype == LLM_I8 && g.act == LLM_ACT_NONE && g.C && !g.C16 && !g.kv &&
+                             !g.ln_x && (g.K / 64) >= 16),
+              "weight_gemm: ksplit2 needs an I8 GEMM into fp32 C with no activation, prologue, "
+              "fp16 copy or KV append, and >= 16 k-steps");
+  a.ksplit2 = g.ksplit2;
   if (g.kv) {
     const KvAppendView& kv = *g.kv;
     LLM_REQUIRE(g.N == 3 * kv.H * kv.D && g.K == kv.H * kv.D, "weight_gemm: kv append shape");

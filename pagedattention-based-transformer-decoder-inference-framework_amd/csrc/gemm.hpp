@@ -59,6 +59,11 @@ struct WeightGemm {
   // ln_b unused) -- the o_proj prologue replacing the attention merge's
   // quantisation (quant_prologue_ok)
   int ln_quant_only = 0;
+  // I8 only, act NONE: 1 = two k slices, each adding its dequantised half
+  // (bias with slice 0) into C with one fp32 atomic add per element.  C must
+  // hold zeros; with exactly two addends the sum is the same bits in either
+  // order (0 + a = a, a + b = b + a), so the result is deterministic.
+  int ksplit2 = 0;
 };
 
 // Input of a LayerNorm when it is not x: embedding rows E[tok[r]] (the decode
@@ -67,6 +72,9 @@ struct LnSource {
   const _Float16* emb = nullptr;
   const int32_t* tok = nullptr;
   int V = 0;
+  // optional (x rows only): the launch writes zeros over the rows it read,
+  // once they are loaded (the next GEMM accumulates into them: ksplit2)
+  float* zero_x = nullptr;
 };
 
 int weight_gemm(const WeightGemm& g, hipStream_t st);

@@ -95,6 +95,7 @@ struct GemmArgs {
   unsigned* seam;
   int seam_n;
   int qdiag;  // tuning build, timing only: bit0 skip the prologue, bit1 no weight loads before it
+  int ksplit2;  // WeightGemm::ksplit2: gridDim.z = 2, each slice atomically adds into C
 };
 
 // LDS image of A for the LayerNorm prologue: row-major 16-byte groups, row
@@ -405,7 +406,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int
       if (!PRO && valid && a.sa) e_scale[e] *= a.sa[m];
       if (valid && a.sw) e_scale[e] *= a.sw[n];
     }
-    e_bias[e] = valid && a.bias ? a.bias[n] : 0.f;
+    e_bias[e] = valid && a.bias && (!a.ksplit2 || bz == 0) ? a.bias[n] : 0.f;
     const bool kvcol = valid && kv.k_pool && n >= hid;
     e_pos[e] = kvcol ? kv.pos[m] : -1;
     e_br[e] = kvcol ? (kv.rows ? kv.rows[m] : m) : -1;
@@ -537,6 +538,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int bx, int by, int
       if (a.acc_out) a.acc_out[(size_t)m * a.N + n] = s;
       y = (float)s * e_scale[e];
       if (a.bias) y = y + e_bias[e];
+      if (a.ksplit2) {  // this k slice's share (bias with slice 0), added into C
+        atomicAdd(a.C + (size_t)m * a.c_ld + n, y);
+        continue;
+      }
     } else {
       float s = 0.f;
 #pragma unroll
@@ -739,7 +744,7 @@ hipError_t launch_gemm(const GemmArgs& a_in, hipStream_t st, int nt_override = 0
   // Infinity Cache); split-K fills them with k slices instead
   if (mrows == 64 && NT == 1 && (a.N + 15) / 16 < 256 && !a.ln_x && !a.partial) mrows = 32;
   if (mrows_override > 0) mrows = mrows_override;
-  const int ks = a.partial ? std::max(1, ks_override) : 1;
+  const int ks = a.partial ? std::max(1, ks_override) : a.ksplit2 ? 2 : 1;
   const int mblocks = (a.M + mrows - 1) / mrows;
   const int tiles = ((a.N + 15) / 16 + NT - 1) / NT * mblocks;
   if (a.xcd_map && (ks < 2 || 8 % ks != 0 || (tiles * ks) % 8 != 0)) a.xcd_map = 0;

@@ -210,6 +210,13 @@ __global__ __launch_bounds__(kRowThreads) void layernorm_rows_kernel(
 #pragma unroll
   for (int i = 0; i < VPT; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
   const float mean = block_sum_fast(s, sh) / (float)cols;
+  if (pp.zero_x && !pp.emb) {  // (after the barrier in block_sum_fast: every thread's loads are done)
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = threadIdx.x + i * kRowThreads;
+      if (c < n4) reinterpret_cast<f32x4*>(pp.zero_x + (size_t)r * cols)[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   float vs = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
