@@ -36,6 +36,10 @@
 
 using namespace llm;
 
+// f[1] = f[0], f[0] = 0 in one device atomic: the fused o_proj's range flag
+// read and cleared (llm_decoder::report_range)
+__global__ void take_flag_kernel(int* f) { f[1] = atomicExch(f, 0); }
+
 namespace {
 
 template <typename T>
@@ -218,8 +222,8 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
     RET_IF(d->a16.alloc(2 * B16 * std::max(hid, inter)));  // act, act2
     RET_IF(d->oacc.alloc((size_t)B * hid));
     LLM_HIP_RET(hipMemset(d->oacc.p, 0, sizeof(long long) * B * hid));
-    RET_IF(d->oflag.alloc(1));
-    LLM_HIP_RET(hipMemset(d->oflag.p, 0, sizeof(int)));
+    RET_IF(d->oflag.alloc(2));  // [0] the flag, [1] take_flag_kernel's result
+    LLM_HIP_RET(hipMemset(d->oflag.p, 0, 2 * sizeof(int)));
     LLM_HIP_RET(hipHostMalloc(reinterpret_cast<void**>(&d->h_oflag), sizeof(int)));
     *d->h_oflag = 0;
   }
@@ -779,24 +783,27 @@ int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t
   if (next_host) {
     LLM_HIP_RET(hipMemcpyAsync(next_host, tokens.p, sizeof(int32_t) * batch,
                                hipMemcpyDeviceToHost, st));
-    if (oflag.p)
-      LLM_HIP_RET(hipMemcpyAsync(h_oflag, oflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (oflag.p) {
+      hipLaunchKernelGGL(take_flag_kernel, dim3(1), dim3(1), 0, st, oflag.p);
+      LLM_HIP_RET(hipGetLastError());
+      LLM_HIP_RET(hipMemcpyAsync(h_oflag, oflag.p + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    }
     LLM_HIP_RET(hipStreamSynchronize(st));
     if (oflag.p) return report_range(*h_oflag);
   }
   return LLM_OK;
 }
 
-// The fused o_proj's range guard (common.hpp oacc_term), reported ONCE: a set
-// flag returns LLM_ERR_RANGE and is cleared, so the steps after it (and the
-// next llm_decoder_sync) succeed unless they clamp again.  range_clamped keeps
-// the fact for llm_decoder_oproj_status until the next begin / generate.
-// Caller holds mu, with the steps' device work complete.
+// The fused o_proj's range guard (common.hpp oacc_term), reported ONCE: the
+// flag is read and cleared in one device atomic (take_flag_kernel), so a
+// clamp by a step still running on another stream is never lost between the
+// read and the clear; a taken flag returns LLM_ERR_RANGE, and the steps after
+// it (and the next llm_decoder_sync) succeed unless they clamp again.
+// range_clamped keeps the fact for llm_decoder_oproj_status until the next
+// begin / generate.  Caller holds mu; `flag` is take_flag_kernel's result.
 int llm_decoder::report_range(int flag) {
   if (!flag) return LLM_OK;
   range_clamped = 1;
-  LLM_HIP_RET(hipMemsetAsync(oflag.p, 0, sizeof(int), stream));
-  LLM_HIP_RET(hipStreamSynchronize(stream));
   return fail(LLM_ERR_RANGE,
               "decoder: a head product of the fused o_proj left its fixed-point range "
               "(|v| > (2^23 - 1) / num_heads, or not finite) and was clamped; the affected "
@@ -806,7 +813,10 @@ int llm_decoder::report_range(int flag) {
 int llm_decoder::oproj_range_status() {
   if (!oflag.p) return LLM_OK;
   int f = 0;
-  LLM_HIP_RET(hipMemcpy(&f, oflag.p, sizeof(int), hipMemcpyDeviceToHost));
+  hipLaunchKernelGGL(take_flag_kernel, dim3(1), dim3(1), 0, stream, oflag.p);
+  LLM_HIP_RET(hipGetLastError());
+  LLM_HIP_RET(hipMemcpyAsync(&f, oflag.p + 1, sizeof(int), hipMemcpyDeviceToHost, stream));
+  LLM_HIP_RET(hipStreamSynchronize(stream));
   return report_range(f);
 }
 

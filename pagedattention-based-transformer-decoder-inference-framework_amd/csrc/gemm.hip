@@ -138,9 +138,10 @@ int llm::weight_gemm(const WeightGemm& g, hipStream_t st) {
   a.sa_out = g.sa_out;
   a.w_keep = g.w_keep;
   LLM_REQUIRE(!g.ksplit2 || (g.dtype == LLM_I8 && g.act == LLM_ACT_NONE && g.C && !g.C16 && !g.kv &&
-                             !g.ln_x && (g.K / 64) >= 16),
-              "weight_gemm: ksplit2 needs an I8 GEMM into fp32 C with no activation, prologue, "
-              "fp16 copy or KV append, and >= 16 k-steps");
+                             !g.ln_x && (g.K / 64) >= 16 && (g.c_cols <= 0 || g.c_cols == g.N) &&
+                             (g.c_ld <= 0 || g.c_ld >= g.N)),
+              "weight_gemm: ksplit2 needs an I8 GEMM into all N columns of fp32 C with no "
+              "activation, prologue, fp16 copy or KV append, and >= 16 k-steps");
   a.ksplit2 = g.ksplit2;
   if (g.kv) {
     const KvAppendView& kv = *g.kv;

@@ -104,6 +104,7 @@ bool KvCache::in_range(int layer, int beam, int head, int tile) const {
 
 void KvCache::set_entry(size_t idx, int32_t page) {
   h_table[idx] = page;
+  lru_forget(idx);  // register_tile re-adds the entries it maps (lru_touch after this)
   if (!dirty_flag[idx]) {
     dirty_flag[idx] = 1;
     dirty.push_back((int64_t)idx);
@@ -183,9 +184,18 @@ void KvCache::lru_touch(size_t idx) {  // KVTileCache::update_lru, kv_tile_cache
   lru_pos[idx] = lru.begin();
 }
 
+void KvCache::lru_forget(size_t idx) {
+  if (lru_pos.empty()) return;
+  auto it = lru_pos.find(idx);
+  if (it == lru_pos.end()) return;
+  lru.erase(it->second);
+  lru_pos.erase(it);
+}
+
 // KVTileCache::evict_if_needed (kv_tile_cache.cpp:89-98): remove the least
-// recently registered entry whose page that frees.  Entries another call has
-// already removed are dropped from the list; entries on a page a forked beam
+// recently registered entry whose page that frees.  Only entries register_tile
+// mapped are in the list (set_entry drops any entry another call rewrites);
+// entries on a page a forked beam
 // still shares stay (evicting them would free nothing, and the reference has
 // no shared pages), so a pool held only by shared pages still reports OOM.
 bool KvCache::lru_evict_one() {
@@ -196,7 +206,7 @@ bool KvCache::lru_evict_one() {
     if (p >= 0 && refcount[p] > 1) continue;
     lru_pos.erase(idx);
     it = lru.erase(it);
-    if (p < 0) continue;
+    if (p < 0) continue;  // (not reached: set_entry drops unmapped entries)
     drop_page(p);
     set_entry(idx, -1);
     return true;
@@ -331,6 +341,7 @@ extern "C" int kv_cache_assign(kv_cache* c, int layer, int beam, int head, int t
   LLM_REQUIRE(page >= -1 && page < k.num_pages, "kv_cache_assign: page out of range");
   const size_t idx = k.index(layer, beam, head, tile);
   const int32_t old = k.h_table[idx];
+  k.lru_forget(idx);  // an entry set by hand is not a registered tile (no eviction candidate)
   if (old == page) return LLM_OK;
   if (page >= 0) {
     // take the page out of the free list if it is there; bump its refcount

@@ -46,12 +46,16 @@ struct KvCache {
   std::mutex mu;
   // kv_cache_set_eviction: LLM_EVICT_LRU makes register_tile evict the least
   // recently registered table entries when the pool is exhausted
-  // (kv_tile_cache.cpp:79-98).  lru: table indices, most recent first; entries
-  // removed by other calls stay in it until an eviction skips them.
+  // (kv_tile_cache.cpp:79-98).  lru: the table indices register_tile mapped,
+  // most recent first.  Any other write of an entry (set_entry: reserve /
+  // prepare_append, assign, remove, release, fork, COW, snapshot load) drops
+  // it from the list, so a page a later caller puts on that entry is never an
+  // eviction candidate unless register_tile maps it again.
   int evict = LLM_EVICT_NONE;
   std::list<size_t> lru;
   std::unordered_map<size_t, std::list<size_t>::iterator> lru_pos;
   void lru_touch(size_t idx);
+  void lru_forget(size_t idx);
   bool lru_evict_one();  // false: nothing left to evict
 
   ~KvCache();

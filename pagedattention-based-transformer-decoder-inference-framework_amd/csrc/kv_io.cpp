@@ -302,6 +302,8 @@ extern "C" int kv_cache_load(kv_cache* c, const char* path) {
   if (int rc = kv_cache_clear(c)) return rc;
   std::unique_lock<std::mutex> g(k.mu);
   k.h_table = s.table;
+  k.lru.clear();  // loaded entries are not registered tiles (kv_cache_impl.hpp lru)
+  k.lru_pos.clear();
   std::fill(k.refcount.begin(), k.refcount.end(), 0);
   for (int32_t t : k.h_table)
     if (t >= 0) k.refcount[t] += 1;

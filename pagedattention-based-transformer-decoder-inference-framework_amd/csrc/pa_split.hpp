@@ -641,6 +641,11 @@ void pa_split_kernel(PaSplitArgs a) {
       }
       ch0 = nsh;
     }
+    // the priority raised at entry falls with the shared-chunk progress; a
+    // workgroup that shares nothing (ragged group, nsh == 0) or whose last
+    // quarter of chunks set nothing drops it here, so it never streams its
+    // private tiles at top priority past the shared-prefix laggards
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (STAMPS) t_shared = __builtin_amdgcn_s_memrealtime();
   if constexpr (STAGES == 1) {

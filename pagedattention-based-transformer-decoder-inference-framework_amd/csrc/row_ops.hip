@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kRowThreads) void quantize_rows_v_kernel(
 // q / out16 in packed-A order when pack.
 template <int VPT>
 __global__ __launch_bounds__(kRowThreads) void layernorm_rows_kernel(
-    const float* __restrict__ x, int rows, int cols, const float* __restrict__ gamma,
+    const float* x /* not restrict: pp.zero_x may point at it (fc2_split) */, int rows, int cols, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float* __restrict__ out, int8_t* __restrict__ q,
     float* __restrict__ inv_scale, _Float16* __restrict__ out16, int pack, LnSource pp) {
   __shared__ float sh[4];

@@ -12,8 +12,8 @@ Rank 0 receives from every peer on its own xGMI link.
 This module is THE multi-rank decode loop: bench.py times it on the GPU ranks
 (HipDecoderStep over the HIP decoder) and tests/test_dist_gloo.py runs the
 same code with the gloo backend on CPU tensors (an oracle-backed step) at world
-sizes 2 and 4, weak and strong (ragged) sharding, bit-exact against one
-process.
+sizes 2, 3 and 4, weak and strong (ragged: padded to the largest shard, one
+gather) sharding, bit-exact against one process.
 """
 from __future__ import annotations
 
@@ -43,18 +43,29 @@ class RowGatherer:
     Per step: t = buffer() (waits for the gather that last used this slot),
     write the step's rows into t, push().  A slot is re-used only after its
     previous gather completed, so step s+1 computes while step s's rows move.
-    With keep=True rank 0 accumulates every gathered step (per-rank tensors
-    concatenated along rows) in `completed`, in step order."""
+    With keep=True rank 0 accumulates every gathered step (per-rank rows
+    concatenated in rank order) in `completed`, in step order.
+
+    Ragged shards (strong scaling at a world size that does not divide the
+    batch) take the SAME collective as equal ones: every rank's buffers hold
+    `pad` = max(shard_rows) rows, the step writes its own rows into the first
+    ones (buffer() returns that prefix view), one torch.distributed gather
+    moves `pad` rows per rank, and rank 0 trims each peer's block to its row
+    count.  So every world size runs the one gather path the single-rank RCCL
+    test and the gloo tests cover; there is no point-to-point branch."""
 
     def __init__(self, shape, dtype, device, world: int, rank: int, shard_rows=None,
                  keep: bool = False):
         import torch
         self.world, self.rank, self.keep = world, rank, keep
-        rows = list(shard_rows) if shard_rows else [shape[0]] * world
-        self.equal = len(set(rows)) == 1
-        self.bufs = [torch.empty(shape, dtype=dtype, device=device) for _ in range(2)]
-        self.recv = [[torch.empty((rows[r],) + tuple(shape[1:]), dtype=dtype, device=device)
-                      for r in range(world)] if rank == 0 else None for _ in range(2)]
+        self.rows = list(shard_rows) if shard_rows else [shape[0]] * world
+        if len(self.rows) != world or self.rows[rank] != shape[0]:
+            raise ValueError("shard_rows must give every rank's row count, this rank's = shape[0]")
+        self.pad = max(self.rows)
+        full = (self.pad,) + tuple(shape[1:])
+        self.bufs = [torch.empty(full, dtype=dtype, device=device) for _ in range(2)]
+        self.recv = [[torch.empty(full, dtype=dtype, device=device) for _ in range(world)]
+                     if rank == 0 else None for _ in range(2)]
         self.works = [None, None]
         self.slot = 0
         self.completed = []
@@ -66,19 +77,21 @@ class RowGatherer:
             self.works[s] = None
             if self.keep and self.rank == 0:
                 import torch
-                self.completed.append(torch.cat(self.recv[s]).clone())
+                self.completed.append(
+                    torch.cat([self.recv[s][r][:n] for r, n in enumerate(self.rows)]).clone())
 
     def buffer(self):
-        """The tensor the next step should write its rows into."""
+        """The tensor the next step should write its rows into (this rank's
+        rows: a prefix of the padded slot)."""
         self._retire(self.slot)
-        return self.bufs[self.slot]
+        return self.bufs[self.slot][:self.rows[self.rank]]
 
     def push(self):
         s = self.slot
         if self.world > 1:
-            self.works[s] = _gather(self.bufs[s], self.recv[s], self.rank, self.equal)
+            self.works[s] = _gather(self.bufs[s], self.recv[s], self.rank)
         elif self.keep:
-            self.completed.append(self.bufs[s].clone())
+            self.completed.append(self.bufs[s][:self.rows[0]].clone())
         self.slot ^= 1
 
     def finish(self):
@@ -91,29 +104,10 @@ class RowGatherer:
 LogitsGatherer = RowGatherer  # the name of the round-1 API
 
 
-def _gather(t, recv, rank, equal):
-    """Equal shards: one torch.distributed gather.  Unequal (ragged strong
-    scaling): point-to-point receives on rank 0, each peer on its own link, and
-    a single send elsewhere."""
+def _gather(t, recv, rank):
+    """One torch.distributed gather of equal-sized (padded) blocks to rank 0."""
     import torch.distributed as dist
-    if equal:
-        return dist.gather(t, recv if rank == 0 else None, dst=0, async_op=True)
-    world = dist.get_world_size()
-    if rank == 0:
-        recv[0].copy_(t)
-        ops = [dist.P2POp(dist.irecv, recv[r], r) for r in range(1, world)]
-    else:
-        ops = [dist.P2POp(dist.isend, t, 0)]
-    return _Works(dist.batch_isend_irecv(ops))
-
-
-class _Works:
-    def __init__(self, reqs):
-        self.reqs = reqs
-
-    def wait(self):
-        for r in self.reqs:
-            r.wait()
+    return dist.gather(t, recv if rank == 0 else None, dst=0, async_op=True)
 
 
 class HipDecoderStep:
@@ -252,13 +246,13 @@ def time_gather(sd: ShardedDecode, iters: int = 10, *, sync: Callable[[], None] 
         sync = torch.cuda.synchronize
     g = sd.g
     buf, recv = g.bufs[0], g.recv[0]
-    _gather(buf, recv, g.rank, g.equal).wait()  # warm the communicator's path
+    _gather(buf, recv, g.rank).wait()  # warm the communicator's path
     sync()
     dist.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(iters):
-        _gather(buf, recv, g.rank, g.equal).wait()
+        _gather(buf, recv, g.rank).wait()
     sync()
     dist.barrier()
     sync()

@@ -1,11 +1,23 @@
 """Shared test helpers: golden fixture loading and page-pool construction."""
 from __future__ import annotations
 
+import json
+import os
 from pathlib import Path
 
 import numpy as np
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
+RECORD_DIR = Path(os.environ.get("LLM_RECORD_DIR",
+                                 Path(__file__).resolve().parents[1] / "gpurun_out"))
+
+
+def record(name: str, **kv) -> None:
+    """Append one JSON line of measured figures to RECORD_DIR/<name>.jsonl (the
+    GPU box's gpurun_out/, copied into profiles/ for the record)."""
+    RECORD_DIR.mkdir(parents=True, exist_ok=True)
+    with open(RECORD_DIR / f"{name}.jsonl", "a") as f:
+        f.write(json.dumps(kv) + "\n")
 
 
 def load_attn_fixture(name: str) -> dict:

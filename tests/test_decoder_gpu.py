@@ -26,7 +26,7 @@ propagate and are held to FREE_RUN_TOL, a drift bound, not a parity bar."""
 import numpy as np
 import pytest
 
-from _util import assert_parity, decoder_kv_at, decoder_kv_to_oracle, rel_err
+from _util import assert_parity, decoder_kv_at, decoder_kv_to_oracle, record, rel_err
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
@@ -193,7 +193,9 @@ def test_int8_decoder_matches_oracle_c1(gpu, oracle):
     print(f"C1 forced lockstep: worst logit rel err {worst:.2e}, int8 flips {n_flips}/{n_vals}")
     # free running (no taps): the same decoder, flips allowed to propagate
     dec.set_taps(0, 0)
-    assert _random_tokens(dec, OracleDecoder(oracle, w, 3), 40, 3, 1000, seed=1) < FREE_RUN_TOL
+    drift = _random_tokens(dec, OracleDecoder(oracle, w, 3), 40, 3, 1000, seed=1)
+    record("free_run", test="c1_random_tokens", step_drift_worst=drift)
+    assert drift < FREE_RUN_TOL, drift
 
 
 def test_int8_decoder_larger_heads(gpu, oracle):
@@ -209,7 +211,8 @@ def test_int8_decoder_larger_heads(gpu, oracle):
                                                  prompts, gen=30, V=512)
     assert n_flips < 1e-3 * n_vals, (n_flips, n_vals)
     dec.set_taps(0, 0)
-    _, _, worst_free = _lockstep(dec, OracleDecoder(oracle, w, 2), prompts, gen=30, V=512)
+    _, ties, worst_free = _lockstep(dec, OracleDecoder(oracle, w, 2), prompts, gen=30, V=512)
+    record("free_run", test="d128_lockstep", step_drift_worst=worst_free, id_differences=ties)
     assert worst_free < FREE_RUN_TOL, worst_free
 
 
@@ -592,11 +595,12 @@ def test_prefill_matches_token_by_token(gpu, oracle):
     rng = np.random.default_rng(3)
     prompts = [rng.integers(0, V, 600).tolist(), rng.integers(0, V, 37).tolist()]
     la, lb, nxt = _prefill_vs_stepping(lambda n: _make_gpu_decoder(w, max_batch=n), prompts, V)
+    errs = [rel_err(lb[r], la[r]) for r in range(2)]
+    gaps = [float((la[r].max() - la[r][nxt[r]]) / np.abs(la[r]).max()) for r in range(2)]
+    record("free_run", test="prefill_vs_token_by_token_int8", logit_err=errs, id_gap_rel=gaps)
     for r in range(2):
-        err = rel_err(lb[r], la[r])
-        assert err < FREE_RUN_TOL, (r, err)
-        gap = la[r].max() - la[r][nxt[r]]
-        assert gap <= FREE_RUN_TOL * np.abs(la[r]).max()
+        assert errs[r] < FREE_RUN_TOL, (r, errs[r])
+        assert gaps[r] <= FREE_RUN_TOL, (r, gaps[r])
 
 
 def test_prefill_decode_kernel_fallback(gpu, oracle):
@@ -637,9 +641,12 @@ def test_prefill_decode_kernel_fallback(gpu, oracle):
         assert la[r].max() - la[r][nxt[r]] <= LOGIT_TOL * np.abs(la[r]).max()
     w = _int8_model(oracle, L=2, H=2, D=256, V=400, S=700, seed=13)
     la, lb, nxt = _prefill_vs_stepping(lambda n: _make_gpu_decoder(w, max_batch=n), prompts, V)
+    errs = [rel_err(lb[r], la[r]) for r in range(2)]
+    gaps = [float((la[r].max() - la[r][nxt[r]]) / np.abs(la[r]).max()) for r in range(2)]
+    record("free_run", test="prefill_decode_kernel_fallback_int8", logit_err=errs, id_gap_rel=gaps)
     for r in range(2):
-        assert rel_err(lb[r], la[r]) < FREE_RUN_TOL, (r, rel_err(lb[r], la[r]))
-        assert la[r].max() - la[r][nxt[r]] <= FREE_RUN_TOL * np.abs(la[r]).max()
+        assert errs[r] < FREE_RUN_TOL, (r, errs[r])
+        assert gaps[r] <= FREE_RUN_TOL, (r, gaps[r])
 
 
 def test_prefill_mfma_fp16_decoder(gpu, oracle):

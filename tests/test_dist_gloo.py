@@ -123,9 +123,11 @@ class _OracleGen:
 @pytest.mark.parametrize("world,mode,gather,staging,global_rows", [
     (2, "weak", "logits", "device", 0),
     (4, "weak", "ids", "host", 0),
-    (2, "strong", "ids", "device", 5),     # ragged: 3 + 2
-    (4, "strong", "logits", "host", 7),    # ragged: 2 + 2 + 2 + 1
-    (4, "strong", "logits", "device", 8),  # equal shards: one collective gather
+    (2, "strong", "ids", "device", 5),     # ragged: 3 + 2, padded to 3 rows per rank
+    (4, "strong", "logits", "host", 7),    # ragged: 2 + 2 + 2 + 1, padded to 2
+    (3, "strong", "logits", "device", 7),  # ragged: 3 + 2 + 2, padded to 3
+    (3, "strong", "ids", "host", 4),       # ragged: 2 + 1 + 1, padded to 2
+    (4, "strong", "logits", "device", 8),  # equal shards: the same collective gather
 ])
 def test_sharded_decode_loop_matches_single_process(world, mode, gather, staging, global_rows):
     import torch.multiprocessing as mp
@@ -157,6 +159,24 @@ def test_sharded_decode_loop_matches_single_process(world, mode, gather, staging
     if gen is not None:
         prompts, got = gen
         assert got == _OracleGen(o, w, len(prompts)).generate_batch(prompts, 4)
+
+
+def test_row_gatherer_pads_ragged_shards():
+    """Ragged shards move as equal padded blocks (one gather): every rank's
+    slot holds max(shard_rows) rows, buffer() is this rank's row prefix, and a
+    shard_rows that does not match the rank's own rows is refused."""
+    import torch
+    sys.path.insert(0, str(PKG))
+    from dist_decode import RowGatherer, shard_sizes
+    rows = shard_sizes(7, 3)  # 3 2 2
+    for rank in range(3):
+        g = RowGatherer((rows[rank], 5), torch.float32, "cpu", 3, rank, rows)
+        assert g.pad == 3 and tuple(g.bufs[0].shape) == (3, 5)
+        assert tuple(g.buffer().shape) == (rows[rank], 5)
+        assert g.buffer().data_ptr() == g.bufs[g.slot].data_ptr()
+        assert (g.recv[0] is not None) == (rank == 0)
+    with pytest.raises(ValueError):
+        RowGatherer((3, 5), torch.float32, "cpu", 3, 1, rows)
 
 
 def test_shard_range_covers_batch():

@@ -244,10 +244,10 @@ def _rccl_worker(port, q):
     with torch.cuda.stream(torch.cuda.Stream()):
         t = torch.arange(3 * V, dtype=torch.float32, device="cuda").view(3, V)
         recv = [torch.full((3, V), -1.0, device="cuda")]
-        dist_decode._gather(t, recv, 0, True).wait()
+        dist_decode._gather(t, recv, 0).wait()
         ids = torch.arange(7, dtype=torch.int32, device="cuda")
         rids = [torch.zeros(7, dtype=torch.int32, device="cuda")]
-        dist_decode._gather(ids, rids, 0, True).wait()
+        dist_decode._gather(ids, rids, 0).wait()
         torch.cuda.synchronize()
         q.put((torch.equal(recv[0], t), torch.equal(rids[0], ids), dist.get_backend()))
     dist.destroy_process_group()

@@ -146,6 +146,34 @@ def test_kv_cache_lru_eviction_vs_reference(gpu):
         llm_capi.check(lib.kv_cache_release(h, 1))
         llm_capi.check(lib.kv_cache_register_tile(h, 1, 1, 1, 1, ctypes.byref(page)))
         assert lib.kv_cache_lookup(h, 0, 0, 0, 0) == -1  # now the oldest, unshared
+        # an entry another call rewrites leaves the recency list: register beam
+        # 0's tiles, release the beam, let the decoder's reserve put pages back
+        # on the same (layer, beam, head, tile) entries, then fill the pool by
+        # register_tile -- the eviction must take a registered tile, never a
+        # reserved one (a stale list entry used to evict it)
+        llm_capi.check(lib.kv_cache_clear(h))
+        for t in range(3):
+            llm_capi.check(lib.kv_cache_register_tile(h, 0, 0, 0, t, ctypes.byref(page)))
+        llm_capi.check(lib.kv_cache_release(h, 0))
+        llm_capi.check(lib.kv_cache_reserve(h, 0, 16))  # tile 0 of beam 0: 2 layers x 2 heads
+        reserved = {(l, 0, hh, 0): lib.kv_cache_lookup(h, l, 0, hh, 0) for l in range(2) for hh in range(2)}
+        assert all(p >= 0 for p in reserved.values())
+        for t in range(2):
+            llm_capi.check(lib.kv_cache_register_tile(h, 1, 1, 0, t, ctypes.byref(page)))
+        assert lib.kv_cache_free_pages(h) == 0
+        llm_capi.check(lib.kv_cache_register_tile(h, 1, 1, 0, 2, ctypes.byref(page)))
+        assert lib.kv_cache_lookup(h, 1, 1, 0, 0) == -1  # the least recently registered
+        assert {k: lib.kv_cache_lookup(h, *k) for k in reserved} == reserved
+        # kv_cache_assign / kv_cache_remove rewrite entries too: a registered
+        # tile re-assigned by hand is no longer an eviction candidate
+        llm_capi.check(lib.kv_cache_assign(h, 1, 1, 0, 1, lib.kv_cache_lookup(h, 1, 1, 0, 1)))
+        p_assigned = lib.kv_cache_lookup(h, 1, 1, 0, 1)
+        llm_capi.check(lib.kv_cache_remove(h, 1, 1, 0, 2))
+        llm_capi.check(lib.kv_cache_register_tile(h, 1, 1, 1, 0, ctypes.byref(page)))  # free page
+        assert lib.kv_cache_register_tile(h, 1, 1, 1, 1, ctypes.byref(page)) == llm_capi.LLM_OK
+        assert lib.kv_cache_lookup(h, 1, 1, 1, 0) == -1  # the only registered entry left
+        assert lib.kv_cache_lookup(h, 1, 1, 0, 1) == p_assigned
+        assert {k: lib.kv_cache_lookup(h, *k) for k in reserved} == reserved
     finally:
         lib.kv_cache_destroy(h)
     # the pybind KVTileCache (kv_tile_cache.hpp:9-41 names)
