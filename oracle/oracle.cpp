@@ -308,16 +308,30 @@ void oracle_i8_gemm(const int8_t* A, const int8_t* W, int32_t* acc_out, float* C
 // LayerNorm<T>::forward restated (decoder/layer_norm.hpp:20-37), T = float:
 // sequential mean, biased variance, inv_std = 1.0 / sqrt(var + eps) (double
 // division of the float sqrt, as written), out = (x-mean)*inv_std*g + b.
+// Test-only control (oracle_set_reduction_order): 1 sums the LayerNorm mean /
+// variance and the decoder's attention dot products in REVERSE index order --
+// the same maths with other fp32 roundings, the kind of difference a parallel
+// reduction makes.  0 (default) is the reference's order; every pinned
+// fixture and every parity test runs at 0.  tests/test_generate_free_run*.py use
+// 1 to measure how far the INT8 decoder drifts from ITSELF free running when
+// only the summation order changes (int8 rounding flips propagating through
+// the KV cache): the yardstick for the GPU's free-running drift.
+static int g_reverse_order = 0;
+
 void oracle_layer_norm(const float* x, int rows, int cols, const float* gamma, const float* beta,
                        float eps, float* out) {
+  const bool rev = g_reverse_order != 0;
   for (int r = 0; r < rows; ++r) {
     const float* in = x + (int64_t)r * cols;
     float* o = out + (int64_t)r * cols;
     float mean = 0;
-    for (int j = 0; j < cols; ++j) mean += in[j];
+    for (int i = 0; i < cols; ++i) mean += in[rev ? cols - 1 - i : i];
     mean /= cols;
     float var = 0;
-    for (int j = 0; j < cols; ++j) var += (in[j] - mean) * (in[j] - mean);
+    for (int i = 0; i < cols; ++i) {
+      const int j = rev ? cols - 1 - i : i;
+      var += (in[j] - mean) * (in[j] - mean);
+    }
     var /= cols;
     const float inv_std = (float)(1.0 / std::sqrt(var + eps));
     for (int j = 0; j < cols; ++j) o[j] = (in[j] - mean) * inv_std * gamma[j] + beta[j];
@@ -616,7 +630,10 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
         for (int t = 0; t < Tb; ++t) {
           const uint16_t* kr = d->k.data() + base + (size_t)t * D;
           float dot = 0.0f;
-          for (int dd = 0; dd < D; ++dd) dot += qv[dd] * half_to_float(kr[dd]);
+          for (int i = 0; i < D; ++i) {
+            const int dd = g_reverse_order ? D - 1 - i : i;
+            dot += qv[dd] * half_to_float(kr[dd]);
+          }
           sc[t] = dot * attn_scale;
         }
         softmax_vec(sc.data(), Tb, 1.0f, pr.data());
@@ -669,6 +686,9 @@ static int decoder_step(void* handle, const int32_t* tokens, const int32_t* pos,
   if (next_out) oracle_argmax_rows(logits.data(), B, m.V, next_out);
   return 0;
 }
+
+void oracle_set_reduction_order(int reverse) { g_reverse_order = reverse ? 1 : 0; }
+int oracle_get_reduction_order() { return g_reverse_order; }
 
 int oracle_num_threads() { return omp_get_max_threads(); }
 // The CPU baseline sets its thread count explicitly (OMP_NUM_THREADS is read

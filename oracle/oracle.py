@@ -114,6 +114,8 @@ class Oracle:
         L.oracle_argmax_rows.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _i32p]
         L.oracle_half_to_float.argtypes = [_u16p, _f32p, ctypes.c_int64]
         L.oracle_float_to_half.argtypes = [_f32p, _u16p, ctypes.c_int64]
+        L.oracle_set_reduction_order.argtypes = [ctypes.c_int]
+        L.oracle_get_reduction_order.restype = ctypes.c_int
         L.oracle_decoder_create.restype = ctypes.c_void_p
         L.oracle_decoder_create.argtypes = [ctypes.POINTER(OracleModel), ctypes.c_int]
         L.oracle_decoder_destroy.argtypes = [ctypes.c_void_p]
@@ -217,6 +219,22 @@ class Oracle:
         out = np.empty(rows, np.int32)
         self.lib.oracle_argmax_rows(_ptr(logits, _f32p), rows, V, _ptr(out, _i32p))
         return out
+
+    def reduction_order(self, reverse: bool):
+        """Context manager (test-only control, oracle.cpp oracle_set_reduction_order):
+        inside it the LayerNorm sums and the decoder's attention dot products
+        run in reverse index order -- same maths, other fp32 roundings."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = self.lib.oracle_get_reduction_order()
+            self.lib.oracle_set_reduction_order(1 if reverse else 0)
+            try:
+                yield
+            finally:
+                self.lib.oracle_set_reduction_order(old)
+        return cm()
 
     def num_threads(self) -> int:
         return int(self.lib.oracle_num_threads())
