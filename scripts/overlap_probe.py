@@ -18,6 +18,8 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "pagedattention-based-transformer-decoder-inference-framework_amd"))
@@ -30,14 +32,39 @@ def cu_mask(bits, ncu=256):
     return words
 
 
-def masked_stream(hip, bits):
+class Masked:
+    """A CU-masked HIP stream (hipExtStreamCreateWithCUMask) wrapped as a torch
+    ExternalStream; destroyed on close (each layout makes only its own pair, so
+    the runtime's hardware queues are never shared between masks)."""
+
+    def __init__(self, hip, bits, ncu):
+        import torch
+        words = cu_mask(bits, ncu)
+        arr = (ctypes.c_uint32 * len(words))(*words)
+        self.hip, self.h = hip, ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(self.h), len(words), arr)
+        assert rc == 0, rc
+        self.s = torch.cuda.ExternalStream(self.h.value)
+
+    def close(self):
+        import torch
+        torch.cuda.synchronize()
+        self.hip.hipStreamDestroy(self.h)
+
+
+def census(cen, st, blocks=2048, spin=2000):
+    """{xcc: set of (se, sh, cu)} the stream's workgroups ran on."""
     import torch
-    words = cu_mask(bits)
-    arr = (ctypes.c_uint32 * len(words))(*words)
-    s = ctypes.c_void_p()
-    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), len(words), arr)
-    assert rc == 0, rc
-    return torch.cuda.ExternalStream(s.value)
+    out = torch.zeros(2 * blocks, dtype=torch.int32, device="cuda")
+    assert cen.census(ctypes.c_void_p(out.data_ptr()), blocks, spin,
+                      ctypes.c_void_p(st.cuda_stream)) == 0
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().astype(np.int64).reshape(-1, 2)
+    res = {}
+    for xcc, hw in o:
+        cu, sh, se = (hw >> 8) & 15, (hw >> 12) & 1, (hw >> 13) & 7
+        res.setdefault(int(xcc) & 15, set()).add((int(se), int(sh), int(cu)))
+    return res
 
 
 def main():
@@ -124,23 +151,51 @@ def main():
     res = {"base_att_all_cus": run(s_all, None, n_att, 0)}
     res["base_att_all_cus_2"] = run(s_all, None, n_att, 0)
     res["base_chain_all_cus"] = run(None, s_all, 0, n_chain)
-    for layout in a.layouts:
-        for k in a.mm_cus:
-            if layout == "low":
-                mm_bits = list(range(k))
-            else:  # every (ncu / k)-th CU
-                mm_bits = list(range(0, ncu, ncu // k))[:k]
-            att_bits = [b for b in range(ncu) if b not in set(mm_bits)]
-            s_att = masked_stream(hip, att_bits)
-            s_mm = masked_stream(hip, mm_bits)
-            key = f"{layout}_{k}"
-            res[key] = {
-                "att_alone": run(s_att, None, n_att, 0),
-                "chain_alone": run(None, s_mm, 0, n_chain),
-                "both": run(s_att, s_mm, n_att, n_chain),
-                "both_2": run(s_att, s_mm, n_att, n_chain),
-            }
-            print(key, json.dumps(res[key]), flush=True)
+    print("base", json.dumps(res), flush=True)
+    cen = ctypes.CDLL(str(ROOT / "scripts/micro/libcensus.so"))
+    cen.census.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    # which mask bits land on which XCC: bits i = r (mod 8), and 32-bit words
+    bit_xcc = {}
+    for r in range(8):
+        m = Masked(hip, [i for i in range(ncu) if i % 8 == r], ncu)
+        c = census(cen, m.s)
+        m.close()
+        print(f"bits = {r} mod 8 -> xcc {sorted(c)} cus {sum(len(v) for v in c.values())}", flush=True)
+        if len(c) == 1:
+            for i in range(r, ncu, 8):
+                bit_xcc[i] = next(iter(c))
+    for w in range(ncu // 32):
+        m = Masked(hip, list(range(32 * w, 32 * w + 32)), ncu)
+        c = census(cen, m.s)
+        m.close()
+        print(f"bits {32 * w}..{32 * w + 31} -> xcc {sorted(c)} cus "
+              f"{sum(len(v) for v in c.values())}", flush=True)
+    if len(bit_xcc) != ncu:
+        print("no per-XCC bit map (bits = r mod 8 did not land on one XCC each)", flush=True)
+        bit_xcc = {i: i % 8 for i in range(ncu)}
+    by_xcc = {x: [i for i in range(ncu) if bit_xcc[i] == x] for x in range(8)}
+    layouts = {
+        "xcd0_all": by_xcc[0],               # one whole XCD for the chains
+        "xcd0_half": by_xcc[0][:len(by_xcc[0]) // 2],
+        "xcd0_quarter": by_xcc[0][:len(by_xcc[0]) // 4],
+        "four_per_xcd": [i for x in range(8) for i in by_xcc[x][:4]],
+    }
+    for key, mm_bits in layouts.items():
+        att_bits = [b for b in range(ncu) if b not in set(mm_bits)]
+        s_att, s_mm = Masked(hip, att_bits, ncu), Masked(hip, mm_bits, ncu)
+        ca, cm = census(cen, s_att.s), census(cen, s_mm.s)
+        res[key] = {
+            "mm_cus": len(mm_bits),
+            "census_att": {x: len(v) for x, v in sorted(ca.items())},
+            "census_mm": {x: len(v) for x, v in sorted(cm.items())},
+            "att_alone": run(s_att.s, None, n_att, 0),
+            "chain_alone": run(None, s_mm.s, 0, n_chain),
+            "both": run(s_att.s, s_mm.s, n_att, n_chain),
+            "both_2": run(s_att.s, s_mm.s, n_att, n_chain),
+        }
+        s_att.close()
+        s_mm.close()
+        print(key, json.dumps(res[key]), flush=True)
     print(json.dumps(res, indent=1))
 
 
