@@ -9,20 +9,33 @@ peak, and cross-checked with SQ_VALU_MFMA_BUSY_CYCLES / 1024 SIMDs / (duration
 * 2.4 GHz).  (rocprofv3's own MfmaUtil divides by GRBM_GUI_ACTIVE, which under
 counter collection spans the serialised profiling window, ~10x the kernel.)
 
-    python scripts/gemm_pmc_summarize.py gpurun_out/gemm_pmc > summary.json"""
+FP16 decoder (C2): SQ_INSTS_VALU_MFMA_MOPS_F16 against the dense FP16 peak
+(~2.5 PF); its o_proj runs inside the attention launch, so three GEMMs per
+layer (qkv, fc1, fc2).
+
+    python scripts/gemm_pmc_summarize.py gpurun_out/gemm_pmc [c3|c5|c2] > summary.json"""
 import csv
 import json
 import sys
 from collections import defaultdict
 from pathlib import Path
 
-PEAK_OPS = 5.0e15
 PEAK_BW = 8.0e12
 SIMDS = 1024
 CLOCK = 2.4e9
-M = 64
-ROLES = ["qkv", "o_proj", "fc1", "fc2"]
-SHAPES = {"qkv": (2048, 6144), "o_proj": (2048, 2048), "fc1": (2048, 8192), "fc2": (8192, 2048)}
+# config -> (rows, hidden, weight dtype, GEMMs per layer in dispatch order)
+CONFIGS = {
+    "c3": (64, 2048, "i8", ["qkv", "o_proj", "fc1", "fc2"]),
+    "c5": (64, 4096, "i8", ["qkv", "o_proj", "fc1", "fc2"]),
+    "c2": (16, 768, "f16", ["qkv", "fc1", "fc2"]),
+}
+PEAKS = {"i8": 5.0e15, "f16": 2.5e15}  # dense MFMA (MI355X_MICROARCH.md)
+MOPS = {"i8": "SQ_INSTS_VALU_MFMA_MOPS_I8", "f16": "SQ_INSTS_VALU_MFMA_MOPS_F16"}
+CFG = sys.argv[2] if len(sys.argv) > 2 else "c3"
+M, HID, DT, ROLES = CONFIGS[CFG]
+PEAK_OPS = PEAKS[DT]
+SHAPES = {"qkv": (HID, 3 * HID), "o_proj": (HID, HID), "fc1": (HID, 4 * HID),
+          "fc2": (4 * HID, HID)}
 
 
 def gemm_dispatches(d, pat, counters):
@@ -45,7 +58,7 @@ def gemm_dispatches(d, pat, counters):
 def by_role(lst):
     res = defaultdict(list)
     for j, e in enumerate(lst):
-        res[ROLES[j % 4]].append(e)
+        res[ROLES[j % len(ROLES)]].append(e)
     return res
 
 
@@ -59,7 +72,7 @@ def main():
     tr = by_role(gemm_dispatches(d / "trace", "*kernel_trace.csv", False))
     cn = {s: by_role(gemm_dispatches(d / s, "*counter_collection.csv", True))
           for s in ("mfma", "mops", "fetch", "write")}
-    res = {"config": "C3 INT8 decoder, 64 rows, eager steps (scripts/prof_gemm.py)",
+    res = {"config": f"{CFG} ({DT} weights), {M} rows, eager steps (scripts/prof_gemm.py)",
            "peaks": {"int8_mfma_ops_per_s": PEAK_OPS, "hbm_bytes_per_s": PEAK_BW},
            "gemms": {}}
     tot_t = tot_w = 0.0
@@ -67,16 +80,18 @@ def main():
         K, N = SHAPES[role]
         t = med([e["dur"] for e in tr[role]])
         kern = tr[role][0]["kernel"] if tr[role] else None
-        mops = med([e.get("SQ_INSTS_VALU_MFMA_MOPS_I8", 0) for e in cn["mops"][role]])
+        mops = med([e.get(MOPS[DT], 0) for e in cn["mops"][role]])
         busy = med([e.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) for e in cn["mfma"][role]])
         fetch = med([e.get("FETCH_SIZE", 0) for e in cn["fetch"][role]])
         write = med([e.get("WRITE_SIZE", 0) for e in cn["write"][role]]) if cn["write"][role] else None
         ops = 2.0 * M * K * N
-        wbytes = K * N + 4 * N  # int8 weights + fp32 column scales
+        es = 1 if DT == "i8" else 2
+        wbytes = K * N * es + (4 * N if DT == "i8" else 0)  # weights (+ fp32 column scales)
         ent = {"kernel": kern, "M": M, "K": K, "N": N, "dispatches": len(tr[role]),
                "median_us": round(t * 1e6, 2),
                "algorithmic_ops": ops,
-               "mfma_ops_counted": mops * 512 if mops is not None else None,
+               "mfma_ops_counted": mops * 512 if mops else None,
+               "mfma_ops_counter": MOPS[DT],
                "achieved_TOPS": round(ops / t / 1e12, 1),
                "mfma_util_vs_peak": round(ops / t / PEAK_OPS, 4),
                "mfma_busy_frac_from_cycles": round(busy / SIMDS / (t * CLOCK), 4) if busy else None,
@@ -87,8 +102,13 @@ def main():
         # attribution: weights once; A (int8 M x K + row scales) once per XCD
         # (every XCD runs workgroups of every row block); output fp32 (qkv: q
         # fp32 + K / V fp16 into the pages)
-        a_bytes = M * K + 4 * M
-        out_b = M * (K * 4 + 2 * K * 2) if role == "qkv" else M * N * 4
+        a_bytes = M * K * es + (4 * M if DT == "i8" else 0)
+        if role == "qkv":
+            out_b = M * (K * 4 + 2 * K * 2)  # q fp32 + K / V fp16 into the pages
+        elif DT == "f16" and role == "fc1":
+            out_b = M * N * 2  # fc2's packed fp16 input
+        else:
+            out_b = M * N * 4
         ent["attribution"] = {
             "weights_B": wbytes, "A_B": a_bytes, "A_xcd_fetches": 8, "output_B": out_b,
             "fetch_model_B": wbytes + 8 * a_bytes,
@@ -102,9 +122,10 @@ def main():
         tot_w += wbytes
     res["per_layer"] = {"gemm_us": round(tot_t * 1e6, 2), "weight_bytes": tot_w,
                         "weight_GBps": round(tot_w / tot_t / 1e9, 1),
-                        "note": "M = 64 rows: 128 int8 ops per weight byte, far below the "
-                                "~625 op/B ridge; these GEMMs are bounded by the weight "
-                                "stream and launch latency, not by the MFMA pipes"}
+                        "note": f"M = {M} rows: {2 * M // (1 if DT == 'i8' else 2)} ops per weight byte, far "
+                                f"below the ~{int(PEAK_OPS / PEAK_BW)} op/B ridge; these GEMMs "
+                                "are bounded by the weight stream and launch latency, not by "
+                                "the MFMA pipes"}
     print(json.dumps(res, indent=1))
 
 

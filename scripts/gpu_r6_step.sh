@@ -20,7 +20,10 @@ for s in ${STEPS:-freerun tune probe bench}; do
       timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --hid 4096 --copies 16 > $O/tune_gemm_c5.txt 2>&1 || exit 1 ;;
     probe)
       timeout -k 10 400 python -u scripts/overlap_probe.py > $O/overlap_probe.txt 2>&1 || { tail -20 $O/overlap_probe.txt; exit 1; }
-      grep -E "^(low|spread)" $O/overlap_probe.txt ;;
+      grep -E "^(base|xcd|four|bits)" $O/overlap_probe.txt || true ;;
+    pmc*)  # GEMM MFMA utilisation + bytes, pmc<config> (default c3)
+      c=${s#pmc}; c=${c:-c3}
+      CFG=$c timeout -k 10 1000 bash scripts/gpu_gemm_pmc.sh || exit 1 ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }

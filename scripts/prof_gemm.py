@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""Driver for GEMM counters: the C3 INT8 decoder (24 L / 16 H / D 128, 64 rows)
-stepped eagerly (LLM_GRAPH=0, so every kernel is its own dispatch) at a short
-context — the weight GEMMs are the same launches as in the 8192-token bench.
-Used under rocprofv3 by scripts/gpu_gemm_pmc.sh."""
+"""Driver for GEMM counters: a bench config's decoder (PROF_CONFIG: c3 INT8 24 L /
+16 H / D 128, 64 rows; c5 INT8 32 H / D 128, 64 rows; c2 FP16 12 H / D 64, 16
+rows) stepped eagerly (LLM_GRAPH=0, so every kernel is its own dispatch) at a
+short context -- the weight GEMMs are the same launches as in the 8192-token
+bench (their shapes do not depend on the context).  PROF_LAYERS (default: the
+config's) limits the layer count, which changes only how many dispatches of
+each GEMM are sampled.  Used under rocprofv3 by scripts/gpu_gemm_pmc.sh."""
 import os
 import sys
 from pathlib import Path
@@ -18,10 +21,11 @@ def main():
     import llm_decoder
     from bench import CONFIGS, make_weights
     torch.cuda.set_device(0)
-    cfg = CONFIGS["c3"]
+    cfg = dict(CONFIGS[os.environ.get("PROF_CONFIG", "c3")])
+    cfg["L"] = int(os.environ.get("PROF_LAYERS", cfg["L"]))
     hid = cfg["H"] * cfg["D"]
-    dec = llm_decoder.INT8Decoder(cfg["L"], cfg["H"], cfg["D"], hid, cfg["V"], 512,
-                                  max_batch=cfg["B"], page_size=cfg["ts"])
+    dec = getattr(llm_decoder, cfg["cls"])(cfg["L"], cfg["H"], cfg["D"], hid, cfg["V"], 512,
+                                           max_batch=cfg["B"], page_size=cfg["ts"])
     dec.set_weights(make_weights(cfg, 1234))
     dec.begin_synthetic(cfg["B"], 256, 1, True)
     for i in range(int(os.environ.get("PROF_STEPS", "3"))):
