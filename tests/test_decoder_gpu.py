@@ -22,7 +22,13 @@ held to the north_star bar:
   * int8 activations: every GPU value within one LSB of the oracle's, flips
     below 1e-3 of all values.
 The free-running tests (no forcing: prompts, generate, prefill) let flips
-propagate and are held to FREE_RUN_TOL, a drift bound, not a parity bar."""
+propagate and are held to FREE_RUN_TOL: the measured drift of these tests
+(round 6, profiles/r06/free_run_generate.jsonl: 1.75e-2 random tokens at C1
+dims, 1.66e-2 lockstep at d 128, 1.2e-2 / 0.94e-2 prefill against token by
+token) plus a margin.  That drift is the INT8 decoder's own: the oracle
+against itself with only its summation order reversed drifts 2.3e-2 at C1
+dims (tests/test_generate_free_run.py); test_generate_free_run_gpu.py holds
+free-running generate to that yardstick."""
 import numpy as np
 import pytest
 
@@ -31,7 +37,7 @@ from _util import assert_parity, decoder_kv_at, decoder_kv_to_oracle, record, re
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
 TIE_TOL = 1e-5
-FREE_RUN_TOL = 5e-2
+FREE_RUN_TOL = 2.5e-2
 
 
 def _torch():

@@ -30,7 +30,7 @@ The bar, per case, on the same weights and prompts:
     FREE_RUN_TOL[case] (the measured figure plus a margin);
   * a row where neither the GPU nor the yardstick flipped (drift < 1e-5) has
     identical ids all the way.
-Measured figures go to gpurun_out/free_run.jsonl (profiles/r06/free_run_generate.json)."""
+Measured figures go to gpurun_out/free_run.jsonl (profiles/r06/free_run_generate.jsonl)."""
 import numpy as np
 import pytest
 
@@ -39,7 +39,7 @@ from _util import record, rel_err
 
 pytestmark = pytest.mark.gpu
 
-# measured worst drift (profiles/r06/free_run_generate.json) plus a margin
+# measured worst drift (profiles/r06/free_run_generate.jsonl) plus a margin
 FREE_RUN_TOL = {"c1_dims": 3e-2, "h16_d128": 9e-2}
 NO_FLIP_TOL = 1e-5
 
