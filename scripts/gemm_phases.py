@@ -25,8 +25,11 @@ lib.i8_gemm_stamps.restype = ctypes.c_int
 lib.i8_gemm_stamps.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + \
     [ctypes.c_void_p] * 5
 M, hid = args.M, args.hid
-shapes = [("qkv_proj", hid, 3 * hid, 2, 64), ("o_proj", hid, hid, 1, 32),
-          ("mlp_fc1", hid, 4 * hid, 2, 64), ("mlp_fc2", 4 * hid, hid, 1, 32)]
+# the decode step's forms: hid 2048 (C3) o_proj / fc2 as 32-row blocks; hid 4096
+# (C5, 256 column tiles) one 64-row block
+nr = 64 if hid >= 4096 else 32
+shapes = [("qkv_proj", hid, 3 * hid, 2, 64), ("o_proj", hid, hid, 1, nr),
+          ("mlp_fc1", hid, 4 * hid, 2, 64), ("mlp_fc2", 4 * hid, hid, 1, nr)]
 for (name, K, N, nt, mr), diag in [(sh, d) for sh in shapes for d in args.diag]:
     W = torch.randint(-128, 128, (K, N), dtype=torch.int8, device="cuda")
     copies = [llm_capi.pack_weights(W, llm_capi.LLM_I8) for _ in range(4)]

@@ -21,9 +21,18 @@ for s in ${STEPS:-freerun tune probe bench}; do
     probe)
       timeout -k 10 400 python -u scripts/overlap_probe.py > $O/overlap_probe.txt 2>&1 || { tail -20 $O/overlap_probe.txt; exit 1; }
       grep -E "^(base|xcd|four|bits)" $O/overlap_probe.txt || true ;;
+    phases)  # in-kernel phase clocks of the GEMM forms (tuning build)
+      for h in 2048 4096; do
+        timeout -k 10 300 python -u scripts/gemm_phases.py --hid $h --diag 0 1 2 3 > $O/gemm_phases_$h.txt 2>&1 || { tail -5 $O/gemm_phases_$h.txt; exit 1; }
+        grep diag $O/gemm_phases_$h.txt
+      done ;;
     pmc*)  # GEMM MFMA utilisation + bytes, pmc<config> (default c3)
       c=${s#pmc}; c=${c:-c3}
       CFG=$c timeout -k 10 1000 bash scripts/gpu_gemm_pmc.sh || exit 1 ;;
+    ov*)  # ov<k>[_<config>]: bench line with LLM_OVERLAP=k (no CPU baseline), A/B
+      k=${s#ov}; c=c3; case $k in *_*) c=${k#*_}; k=${k%%_*};; esac
+      LLM_OVERLAP=$k timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/ov${k}_$c.json 2> $O/ov${k}_$c.err || { tail -20 $O/ov${k}_$c.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/ov${k}_$c.json'));print('ov$k $c',d['value'],d['ms_per_step'],d.get('ms_per_step_median_hip_events'))" ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
