@@ -36,12 +36,6 @@
 
 using namespace llm;
 
-// Overlap mode defaults (llm_decoder::overlap_step): CUs per XCD given to the
-// GEMM-chain stream (LLM_OVERLAP; 0 = off) and the mean context a step needs
-// before its attention is long enough to hide a chain (LLM_OVERLAP_MIN_CTX).
-constexpr int kOverlapCusPerXcd = 0;
-constexpr int kOverlapMinCtx = 2048;
-
 // f[1] = f[0], f[0] = 0 in one device atomic: the fused o_proj's range flag
 // read and cleared (llm_decoder::report_range)
 __global__ void take_flag_kernel(int* f) { f[1] = atomicExch(f, 0); }
@@ -142,21 +136,7 @@ struct llm_decoder {
     if (graph) (void)hipGraphExecDestroy(graph);
     if (kv) kv_cache_destroy(kv);
     if (stream) (void)hipStreamDestroy(stream);
-    for (hipEvent_t e : ov_ev) (void)hipEventDestroy(e);
-    if (s_att) (void)hipStreamDestroy(s_att);
-    if (s_mm) (void)hipStreamDestroy(s_mm);
   }
-
-  // Overlap mode (row halves on CU-partitioned streams, enqueue_step_overlap):
-  // ov_k = CUs per XCD of the GEMM-chain partition (0: off; LLM_OVERLAP),
-  // s_att / s_mm the attention / chain streams, ov_ev the step's events.
-  int ov_k = 0;
-  int ov_min_ctx = 0;
-  hipStream_t s_att = nullptr, s_mm = nullptr;
-  std::vector<hipEvent_t> ov_ev;
-  bool overlap_step() const;
-  int ensure_overlap();
-  int enqueue_step_overlap(hipStream_t st);
 
   int row_group = 1;  // beam width of llm_decoder_begin_beams (beam-aware attention)
   // sampling (llm_decoder_set_sampling); greedy argmax by default, as the
@@ -266,8 +246,6 @@ extern "C" int llm_decoder_create(const llm_decoder_config* cfg_in, llm_decoder*
   // C4 -5 %, C3 -0.5..+1 %: the branches do not overlap usefully, and a
   // saturating KV scan slows the other half's glue 4-8x).
   d->use_graph = env_int("LLM_GRAPH", 1) != 0;
-  d->ov_k = std::max(0, std::min(16, env_int("LLM_OVERLAP", kOverlapCusPerXcd)));
-  d->ov_min_ctx = env_int("LLM_OVERLAP_MIN_CTX", kOverlapMinCtx);
   d->h_pos.assign(B, 0);
   *out = d.release();
   return LLM_OK;
@@ -758,96 +736,6 @@ int llm_decoder::enqueue_step(hipStream_t st) {
   return step_tail(st, 0, batch);
 }
 
-// ---------------------------------------------------------------------------
-// Overlap mode.  An INT8 step at C3 / C5 shapes is ~91 % attention (HBM-bound,
-// 6.7 TB/s) and ~9 % weight GEMMs + row kernels, which are latency-bound
-// (fixed costs, broadcast activation reads) and use the HBM little.  The rows
-// of a step are independent, so the step runs as two row halves A and B
-// whose chains interleave: half A's o_proj .. fc2 and next-layer LayerNorm +
-// qkv run while half B's attention streams, and the other way round.  The
-// two kinds of work go to two streams whose CU masks split every XCD
-// (hipExtStreamCreateWithCUMask): the chain stream gets ov_k CUs of each XCD,
-// the attention stream the rest.  A mask cannot leave an XCD out -- an XCD
-// without a bit is given all its CUs -- and mask bit i lies on XCD i % 8
-// (scripts/overlap_probe.py census, profiles/r06/overlap_probe.txt), so the
-// chain mask is bits [0, 8 ov_k).  Captured graphs do not keep stream CU
-// masks, so this mode launches eagerly (a 16 ms step issues in ~1.5 ms of
-// host time).  Every row computes exactly what the one-stream step computes;
-// only the attention split count (planned per 32-row launch) differs.
-// ---------------------------------------------------------------------------
-bool llm_decoder::overlap_step() const {
-  if (ov_k <= 0 || wdtype != LLM_I8 || row_group != 1 || batch < 32) return false;
-  long long ctx_sum = 0;
-  for (int b = 0; b < batch; ++b) ctx_sum += h_pos[b] + 1;
-  return ctx_sum >= (long long)ov_min_ctx * batch;
-}
-
-int llm_decoder::ensure_overlap() {
-  if (s_att) return LLM_OK;
-  int dev = 0, cus = 0;
-  LLM_HIP_RET(hipGetDevice(&dev));
-  LLM_HIP_RET(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  LLM_REQUIRE(cus >= 16 * ov_k && cus % 8 == 0, "decoder: overlap mode: CU count");
-  const int words = (cus + 31) / 32;
-  std::vector<uint32_t> m_att(words, 0u), m_mm(words, 0u);
-  for (int i = 0; i < cus; ++i) (i < 8 * ov_k ? m_mm : m_att)[i / 32] |= 1u << (i % 32);
-  LLM_HIP_RET(hipExtStreamCreateWithCUMask(&s_att, (uint32_t)words, m_att.data()));
-  LLM_HIP_RET(hipExtStreamCreateWithCUMask(&s_mm, (uint32_t)words, m_mm.data()));
-  ov_ev.assign(4 * (size_t)L + 2, nullptr);
-  for (hipEvent_t& e : ov_ev) LLM_HIP_RET(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  return LLM_OK;
-}
-
-// One decode step of all active rows in overlap mode (eager).  Events per
-// layer l: QA / QB (half's qkv done: its attention may start), TA / TB (half's
-// attention done: its o_proj may start); each wait is issued after its record.
-int llm_decoder::enqueue_step_overlap(hipStream_t st) {
-  RET_IF(ensure_overlap());
-  const int nA = (batch / 2 + 15) / 16 * 16;  // 16-row packed-A tiles
-  const int nB = batch - nA;
-  Rows RA = step_rows(0, nA, attn_ws.p), RB = step_rows(nA, nB, attn_ws.p);
-  RA.wgm_quant = wgm_quant_ok(RA);
-  RB.wgm_quant = wgm_quant_ok(RB);
-  hipEvent_t* QA = &ov_ev[0];
-  hipEvent_t* QB = QA + L;
-  hipEvent_t* TA = QB + L;
-  hipEvent_t* TB = TA + L;
-  hipEvent_t e0 = ov_ev[4 * (size_t)L], e1 = ov_ev[4 * (size_t)L + 1];
-  LLM_HIP_RET(hipEventRecord(e0, st));
-  LLM_HIP_RET(hipStreamWaitEvent(s_att, e0, 0));
-  LLM_HIP_RET(hipStreamWaitEvent(s_mm, e0, 0));
-  RET_IF(step_head(s_mm, 0, nA));
-  RET_IF(layer_pre(0, s_mm, RA));
-  LLM_HIP_RET(hipEventRecord(QA[0], s_mm));
-  RET_IF(step_head(s_mm, nA, nB));
-  RET_IF(layer_pre(0, s_mm, RB));
-  LLM_HIP_RET(hipEventRecord(QB[0], s_mm));
-  for (int l = 0; l < L; ++l) {
-    LLM_HIP_RET(hipStreamWaitEvent(s_att, QA[l], 0));
-    RET_IF(layer_attn(l, s_att, RA));
-    LLM_HIP_RET(hipEventRecord(TA[l], s_att));
-    LLM_HIP_RET(hipStreamWaitEvent(s_att, QB[l], 0));
-    RET_IF(layer_attn(l, s_att, RB));
-    LLM_HIP_RET(hipEventRecord(TB[l], s_att));
-    LLM_HIP_RET(hipStreamWaitEvent(s_mm, TA[l], 0));
-    RET_IF(layer_post(l, s_mm, RA));
-    if (l + 1 < L) {
-      RET_IF(layer_pre(l + 1, s_mm, RA));
-      LLM_HIP_RET(hipEventRecord(QA[l + 1], s_mm));
-    }
-    LLM_HIP_RET(hipStreamWaitEvent(s_mm, TB[l], 0));
-    RET_IF(layer_post(l, s_mm, RB));
-    if (l + 1 < L) {
-      RET_IF(layer_pre(l + 1, s_mm, RB));
-      LLM_HIP_RET(hipEventRecord(QB[l + 1], s_mm));
-    }
-  }
-  RET_IF(step_tail(s_mm, 0, batch));  // the LM head over every row (x rows contiguous)
-  LLM_HIP_RET(hipEventRecord(e1, s_mm));
-  LLM_HIP_RET(hipStreamWaitEvent(st, e1, 0));
-  return LLM_OK;
-}
-
 int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t* next_host,
                           hipStream_t st) {
   LLM_REQUIRE(weights_ready, "decoder: weights not loaded");
@@ -867,9 +755,7 @@ int llm_decoder::run_step(const int32_t* tokens_host, float* logits_dev, int32_t
     LLM_HIP_RET(hipMemcpyAsync(tokens.p, tokens_host, sizeof(int32_t) * batch,
                                hipMemcpyHostToDevice, st));
   }
-  if (overlap_step()) {
-    RET_IF(enqueue_step_overlap(st));
-  } else if (!use_graph) {
+  if (!use_graph) {
     RET_IF(enqueue_step(st));
   } else {
     if (graph_batch != batch) {

@@ -33,6 +33,11 @@ for s in ${STEPS:-freerun tune probe bench}; do
       k=${s#ov}; c=c3; case $k in *_*) c=${k#*_}; k=${k%%_*};; esac
       LLM_OVERLAP=$k timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/ov${k}_$c.json 2> $O/ov${k}_$c.err || { tail -20 $O/ov${k}_$c.err; exit 1; }
       python -c "import json;d=json.load(open('$O/ov${k}_$c.json'));print('ov$k $c',d['value'],d['ms_per_step'],d.get('ms_per_step_median_hip_events'))" ;;
+    trace*)  # trace<k>: kernel trace of the C3 bench with LLM_OVERLAP=k
+      k=${s#trace}
+      LLM_OVERLAP=$k bash scripts/trace_step.sh ov$k --config c3 || exit 1
+      f=$(ls gpurun_out/trace_ov$k/*kernel_trace.csv | head -1)
+      if [ "$k" = 0 ]; then python scripts/analyze_trace.py $f | head -14; else python scripts/overlap_timeline.py $f; fi ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
