@@ -15,6 +15,9 @@ for s in ${STEPS:-freerun tune probe bench}; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
       rc=$?; grep -E "FAILED|ERROR" $O/gpu_tests.log | head -20; tail -2 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    tunent)  # the 3 / 4 column-tile forms (tuning build) at C3 and C5 shapes
+      timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --copies 64 --nts 2 3 4 > $O/tune_gemm_nt_c3.txt 2>&1 || exit 1
+      timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --hid 4096 --copies 16 --nts 2 3 4 > $O/tune_gemm_nt_c5.txt 2>&1 || exit 1 ;;
     tune)
       timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --copies 64 > $O/tune_gemm_c3.txt 2>&1 || exit 1
       timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --hid 4096 --copies 16 > $O/tune_gemm_c5.txt 2>&1 || exit 1 ;;
@@ -38,6 +41,10 @@ for s in ${STEPS:-freerun tune probe bench}; do
       LLM_OVERLAP=$k bash scripts/trace_step.sh ov$k --config c3 || exit 1
       f=$(ls gpurun_out/trace_ov$k/*kernel_trace.csv | head -1)
       if [ "$k" = 0 ]; then python scripts/analyze_trace.py $f | head -14; else python scripts/overlap_timeline.py $f; fi ;;
+    wgm*)  # wgm<P>_<NS>[_<config>]: bench line with LLM_WGM_PARTS=P LLM_WGM_NSPLIT=NS
+      v=${s#wgm}; P=${v%%_*}; r=${v#*_}; NS=${r%%_*}; c=c2; case $r in *_*) c=${r#*_};; esac
+      LLM_WGM_PARTS=$P LLM_WGM_NSPLIT=$NS timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $O/wgm${P}_${NS}_$c.json 2> $O/wgm${P}_${NS}_$c.err || { tail -20 $O/wgm${P}_${NS}_$c.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/wgm${P}_${NS}_$c.json'));r=d['roofline'];print('wgm P=$P NS=$NS $c',d['value'],d['ms_per_step'],r.get('launch_us'),r.get('frac'))" ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
