@@ -45,6 +45,8 @@ for s in ${STEPS:-freerun tune probe bench}; do
       v=${s#wgm}; P=${v%%_*}; r=${v#*_}; NS=${r%%_*}; c=c2; case $r in *_*) c=${r#*_};; esac
       LLM_WGM_PARTS=$P LLM_WGM_NSPLIT=$NS timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $O/wgm${P}_${NS}_$c.json 2> $O/wgm${P}_${NS}_$c.err || { tail -20 $O/wgm${P}_${NS}_$c.err; exit 1; }
       python -c "import json;d=json.load(open('$O/wgm${P}_${NS}_$c.json'));r=d['roofline'];print('wgm P=$P NS=$NS $c',d['value'],d['ms_per_step'],r.get('launch_us'),r.get('frac'))" ;;
+    ab*)  # ab<config>: same-box A/B of ab_base/ (scripts/build_ab_base.sh) against the tree
+      c=${s#ab}; STEPS=30 AB_DIR=ab_base CONFIGS=$c ROUNDS=${ROUNDS:-2} timeout -k 10 1000 bash scripts/gpu_lib_ab.sh || exit 1 ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
