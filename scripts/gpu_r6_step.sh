@@ -15,6 +15,20 @@ for s in ${STEPS:-freerun tune probe bench}; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
       rc=$?; grep -E "FAILED|ERROR" $O/gpu_tests.log | head -20; tail -2 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    pmcatt*)  # pmcatt<config>: attention PMC traffic of the decoder's own launch
+      c=${s#pmcatt}
+      DEC=--decoder timeout -k 10 900 bash scripts/gpu_pmc.sh $c || exit 1
+      python -c "import json;d=json.load(open('gpurun_out/pmc_attention_$c.json'));print('$c', {k: d[k] for k in list(d)[:8]})" ;;
+    record*)  # record<config>: the full bench line (CPU baseline included) + the step's kernel trace
+      c=${s#record}
+      timeout -k 10 600 python bench.py --config $c > $O/r06_bench_$c.json 2> $O/r06_bench_$c.err || { tail -20 $O/r06_bench_$c.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/r06_bench_$c.json'));print('$c',d['value'],d['ms_per_step'],d['roofline']['frac'],d['cpu_baseline']['value'])"
+      bash scripts/trace_step.sh $c --config $c || exit 1
+      f=$(ls gpurun_out/trace_$c/*kernel_trace.csv | head -1)
+      python scripts/analyze_trace.py $f --by-grid > $O/step_timeline_$c.txt && head -4 $O/step_timeline_$c.txt ;;
     tunent)  # the 3 / 4 column-tile forms (tuning build) at C3 and C5 shapes
       timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --copies 64 --nts 2 3 4 > $O/tune_gemm_nt_c3.txt 2>&1 || exit 1
       timeout -k 10 300 python -u scripts/tune_gemm.py --M 64 --hid 4096 --copies 16 --nts 2 3 4 > $O/tune_gemm_nt_c5.txt 2>&1 || exit 1 ;;
