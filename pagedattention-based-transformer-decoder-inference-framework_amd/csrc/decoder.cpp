@@ -537,9 +537,13 @@ bool llm_decoder::wgm_quant_ok(const Rows& R) {
 // zeros over the rows after loading them.  Standalone (scripts/tune_gemm_sk.py,
 // profiles/r05/gemm_small_m.txt): fc2 at M = 8 6.86 -> 5.67 us, M = 16 7.53 ->
 // 5.95 us.
+// Round 6: also at 33..64 rows when inter >= 16384 (C5's fc2, K 16384): every
+// workgroup of the one-slice form reads all of A, 1 MB, the k slices half of
+// it (gemm_impl.hpp narrow_decode_tile).
 bool llm_decoder::fc2_split(const Rows& R) const {
-  return wdtype == LLM_I8 && R.prefill_row < 0 && R.n <= 16 && !ln_fusable(wdtype, R.n, hid) &&
-         inter / 64 >= 16;
+  return wdtype == LLM_I8 && R.prefill_row < 0 &&
+         (R.n <= 16 || (R.n > 32 && R.n <= 64 && inter >= 16384)) &&
+         !ln_fusable(wdtype, R.n, hid) && inter / 64 >= 16;
 }
 
 int llm_decoder::layer_attn(int l, hipStream_t st, const Rows& R, PaPlan* plan) {

@@ -716,8 +716,18 @@ inline bool narrow_tile_for(int M, int N, int K, TileChoice& t) {
   }
   return false;
 }
+// fc2 as two k slices at 33..64 rows (decoder.cpp fc2_split: C5's K 16384):
+// 2 column tiles x 64 rows x 8 waves per slice, 128 x 2 = 256 workgroups in
+// one round, each reading half of A (512 KB instead of the 1-tile form's
+// 1 MB per workgroup).  Same box, C5 (profiles/r06/c5_fc2_k2_ab.txt):
+// 1,441.1 / 1,442.5 against 1,438.9 / 1,439.5 tok/s; one column tile per
+// slice (512 workgroups, two rounds) 1,435.4 / 1,437.5.
 inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
   if ((a.ln_x && a.ln_g) || a.partial) return false;
+  if (a.ksplit2 && a.M > 32 && a.M <= 64) {
+    t = TileChoice{2, 8, 64};
+    return true;
+  }
   return narrow_tile_for(a.M, a.N, a.KS * kstep, t);
 }
 

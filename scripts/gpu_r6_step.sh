@@ -61,6 +61,10 @@ for s in ${STEPS:-freerun tune probe bench}; do
       python -c "import json;d=json.load(open('$O/wgm${P}_${NS}_$c.json'));r=d['roofline'];print('wgm P=$P NS=$NS $c',d['value'],d['ms_per_step'],r.get('launch_us'),r.get('frac'))" ;;
     ab*)  # ab<config>: same-box A/B of ab_base/ (scripts/build_ab_base.sh) against the tree
       c=${s#ab}; STEPS=30 AB_DIR=ab_base CONFIGS=$c ROUNDS=${ROUNDS:-2} timeout -k 10 1000 bash scripts/gpu_lib_ab.sh || exit 1 ;;
+    k2nt*)  # k2nt<NT>[_<config>]: bench line with LLM_FC2_K2_NT=NT (fc2 as two k slices at 64 rows)
+      v=${s#k2nt}; k=${v%%_*}; c=c5; case $v in *_*) c=${v#*_};; esac
+      LLM_FC2_K2_NT=$k timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/k2nt${k}_$c.json 2> $O/k2nt${k}_$c.err || { tail -20 $O/k2nt${k}_$c.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/k2nt${k}_$c.json'));print('k2nt$k $c',d['value'],d['ms_per_step'])" ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
