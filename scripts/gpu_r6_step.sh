@@ -8,6 +8,10 @@ mkdir -p gpurun_out/r06
 O=gpurun_out/r06
 for s in ${STEPS:-freerun tune probe bench}; do
   case $s in
+    t:*)  # t:<test file stem>[,<stem>...]: those GPU test files only
+      f=""; for x in $(echo ${s#t:} | tr , ' '); do f="$f tests/$x.py"; done
+      timeout -k 10 900 python -u -m pytest $f -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread > $O/tests_subset.log 2>&1
+      rc=$?; grep -E "FAILED|ERROR" $O/tests_subset.log | head; tail -2 $O/tests_subset.log; [ $rc -eq 0 ] || exit $rc ;;
     freerun)  # measurement: every test runs (no -x); a failure does not end the session
       timeout -k 10 900 python -u -m pytest tests/test_generate_free_run_gpu.py tests/test_decoder_gpu.py -m gpu -v -s -p no:cacheprovider --timeout 300 --timeout-method thread > $O/free_run_tests.log 2>&1
       rc=$?; grep -E "FAILED|passed|failed" $O/free_run_tests.log | tail -8
@@ -65,6 +69,10 @@ for s in ${STEPS:-freerun tune probe bench}; do
       v=${s#k2nt}; k=${v%%_*}; c=c5; case $v in *_*) c=${v#*_};; esac
       LLM_FC2_K2_NT=$k timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/k2nt${k}_$c.json 2> $O/k2nt${k}_$c.err || { tail -20 $O/k2nt${k}_$c.err; exit 1; }
       python -c "import json;d=json.load(open('$O/k2nt${k}_$c.json'));print('k2nt$k $c',d['value'],d['ms_per_step'])" ;;
+    env:*)  # env:<VAR>=<v>:<config>: bench line under that variable (A/B)
+      v=${s#env:}; kv=${v%%:*}; c=${v#*:}
+      env $kv timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/env_$c.json 2> $O/env_$c.err || { tail -20 $O/env_$c.err; exit 1; }
+      python -c "import json;d=json.load(open('$O/env_$c.json'));print('$kv $c',d['value'],d['ms_per_step'])" ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
       timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 1; }
