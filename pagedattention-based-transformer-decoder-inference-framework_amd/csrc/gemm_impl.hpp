@@ -722,7 +722,8 @@ inline bool narrow_tile_for(int M, int N, int K, TileChoice& t) {
 // 1 MB per workgroup).  Same box, C5 (profiles/r06/c5_fc2_k2_ab.txt):
 // 1,441.1 / 1,442.5 against 1,438.9 / 1,439.5 tok/s; one column tile per
 // slice (512 workgroups, two rounds) 1,435.4 / 1,437.5.  At C3 (K 8192) no
-// tile of it beats the one-slice 16-row form (profiles/r06/c3_fc2_k2_ab.txt).
+// tile of it beats the one-slice 16-row form (profiles/r06/c3_fc2_k2_ab.txt),
+// nor at C4's 32 rows (c4_fc2_k2_ab.txt).
 inline bool narrow_decode_tile(const GemmArgs& a, int kstep, TileChoice& t) {
   if ((a.ln_x && a.ln_g) || a.partial) return false;
   if (a.ksplit2 && a.M > 32 && a.M <= 64) {
