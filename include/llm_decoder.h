@@ -299,9 +299,12 @@ int kv_cache_register_tile(kv_cache* c, int layer, int beam, int head, int tile,
  * needs a page when none is free takes one by removing the least recently
  * registered tile whose page that frees (an entry on a page a forked beam
  * still shares is kept) -- the reference's semantics, so an evicted tile of a
- * live sequence reads as missing (masked) afterwards.  Only tiles registered
- * through kv_cache_register_tile are candidates; the decoder's own pages
- * (reserve / append) never are.  Switching the policy keeps the recency list. */
+ * live sequence reads as missing (masked) afterwards.  Only entries whose
+ * page kv_cache_register_tile mapped are candidates: any other call that
+ * writes an entry (reserve / the decoder's append, assign -- even with its
+ * current page --, remove, release, fork, copy-on-write, a snapshot load)
+ * takes it off the recency list, so the decoder's own pages never are.
+ * Switching the policy keeps the recency list. */
 #define LLM_EVICT_NONE 0
 #define LLM_EVICT_LRU 1
 int kv_cache_set_eviction(kv_cache* c, int policy);
