@@ -1,12 +1,14 @@
 #!/bin/bash
 # Round-6 GPU session driver: each STEPS word runs one measured step into
 # gpurun_out/r06/ (every step under its own time limit; the first failure ends
-# the session).  STEPS="freerun tune probe bench" by default.
+# the session).  STEPS="tests smoke bench" by default.  The round's experiment
+# switches (LLM_OVERLAP, LLM_WGM_PARTS, LLM_FC2_K2_NT) were measured through
+# "env:<VAR>=<v>:<config>" and removed with the code.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r06
 O=gpurun_out/r06
-for s in ${STEPS:-freerun tune probe bench}; do
+for s in ${STEPS:-tests smoke bench}; do
   case $s in
     t:*)  # t:<test file stem>[,<stem>...]: those GPU test files only
       f=""; for x in $(echo ${s#t:} | tr , ' '); do f="$f tests/$x.py"; done
@@ -50,25 +52,13 @@ for s in ${STEPS:-freerun tune probe bench}; do
     pmc*)  # GEMM MFMA utilisation + bytes, pmc<config> (default c3)
       c=${s#pmc}; c=${c:-c3}
       CFG=$c timeout -k 10 1000 bash scripts/gpu_gemm_pmc.sh || exit 1 ;;
-    ov*)  # ov<k>[_<config>]: bench line with LLM_OVERLAP=k (no CPU baseline), A/B
-      k=${s#ov}; c=c3; case $k in *_*) c=${k#*_}; k=${k%%_*};; esac
-      LLM_OVERLAP=$k timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/ov${k}_$c.json 2> $O/ov${k}_$c.err || { tail -20 $O/ov${k}_$c.err; exit 1; }
-      python -c "import json;d=json.load(open('$O/ov${k}_$c.json'));print('ov$k $c',d['value'],d['ms_per_step'],d.get('ms_per_step_median_hip_events'))" ;;
-    trace*)  # trace<k>: kernel trace of the C3 bench with LLM_OVERLAP=k
-      k=${s#trace}
-      LLM_OVERLAP=$k bash scripts/trace_step.sh ov$k --config c3 || exit 1
-      f=$(ls gpurun_out/trace_ov$k/*kernel_trace.csv | head -1)
-      if [ "$k" = 0 ]; then python scripts/analyze_trace.py $f | head -14; else python scripts/overlap_timeline.py $f; fi ;;
-    wgm*)  # wgm<P>_<NS>[_<config>]: bench line with LLM_WGM_PARTS=P LLM_WGM_NSPLIT=NS
-      v=${s#wgm}; P=${v%%_*}; r=${v#*_}; NS=${r%%_*}; c=c2; case $r in *_*) c=${r#*_};; esac
-      LLM_WGM_PARTS=$P LLM_WGM_NSPLIT=$NS timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $O/wgm${P}_${NS}_$c.json 2> $O/wgm${P}_${NS}_$c.err || { tail -20 $O/wgm${P}_${NS}_$c.err; exit 1; }
-      python -c "import json;d=json.load(open('$O/wgm${P}_${NS}_$c.json'));r=d['roofline'];print('wgm P=$P NS=$NS $c',d['value'],d['ms_per_step'],r.get('launch_us'),r.get('frac'))" ;;
+    trace*)  # trace<config>: kernel trace of the bench step, per-kernel timeline
+      c=${s#trace}; c=${c:-c3}
+      bash scripts/trace_step.sh $c --config $c || exit 1
+      f=$(ls gpurun_out/trace_$c/*kernel_trace.csv | head -1)
+      python scripts/analyze_trace.py $f --by-grid | head -14 ;;
     ab*)  # ab<config>: same-box A/B of ab_base/ (scripts/build_ab_base.sh) against the tree
       c=${s#ab}; STEPS=30 AB_DIR=ab_base CONFIGS=$c ROUNDS=${ROUNDS:-2} timeout -k 10 1000 bash scripts/gpu_lib_ab.sh || exit 1 ;;
-    k2nt*)  # k2nt<NT>[_<config>]: bench line with LLM_FC2_K2_NT=NT (fc2 as two k slices at 64 rows)
-      v=${s#k2nt}; k=${v%%_*}; c=c5; case $v in *_*) c=${v#*_};; esac
-      LLM_FC2_K2_NT=$k timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/k2nt${k}_$c.json 2> $O/k2nt${k}_$c.err || { tail -20 $O/k2nt${k}_$c.err; exit 1; }
-      python -c "import json;d=json.load(open('$O/k2nt${k}_$c.json'));print('k2nt$k $c',d['value'],d['ms_per_step'])" ;;
     env:*)  # env:<VAR>=<v>:<config>: bench line under that variable (A/B)
       v=${s#env:}; kv=${v%%:*}; c=${v#*:}
       env $kv timeout -k 10 400 python bench.py --config $c --no-cpu-baseline > $O/env_$c.json 2> $O/env_$c.err || { tail -20 $O/env_$c.err; exit 1; }
