@@ -3,7 +3,7 @@
 # gpurun_out/r06/ (every step under its own time limit; the first failure ends
 # the session).  STEPS="tests smoke bench" by default.  The round's experiment
 # switches (LLM_OVERLAP, LLM_WGM_PARTS, LLM_FC2_K2_NT) were measured through
-# "env:<VAR>=<v>:<config>" and removed with the code (DESIGN §9).
+# "env:<VAR>=<v>:<config>" and removed with the code (DESIGN §10).
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r06
