@@ -96,6 +96,11 @@ struct PaSplitArgs {
   // entry, at the first KV load, after the shared-prefix chunks, at exit, and
   // the wave's HW_ID (CU / SIMD / XCC placement): stamps[wid * 5 + 0..4]
   unsigned long long* stamps;
+  // BEAM: split-major workgroup order (blockIdx = s * groups * H + group * H +
+  // head) instead of ((group * H + head) * nsplit + s).  A CU's 4 resident
+  // workgroups (blockIdx b, b + 256, b + 512, b + 768 at C4) are then 4 split
+  // pairs of 4 (group, head)s rather than 4 sequence pairs.
+  int smaj;  // (last: the earlier fields keep their kernel-argument offsets)
 };
 
 constexpr int kWgmMaxSplits = 8;  // one merge batch (pa_merge_row_kernel's kMergeBatch)
@@ -206,8 +211,9 @@ void pa_split_kernel(PaSplitArgs a) {
   const int G = BEAM ? 4 : WGM ? 1 : a.group;
   const int gi = wid % G;  // row within the group (fastest: adjacent waves)
   const int rest = wid / G;
-  const int s = rest % a.nsplit;
-  const int gh = rest / a.nsplit;
+  const int GH = BEAM && a.smaj ? ((a.B + 3) / 4) * a.H : 1;
+  const int s = BEAM && a.smaj ? rest / GH : rest % a.nsplit;
+  const int gh = BEAM && a.smaj ? rest % GH : rest / a.nsplit;
   const int h = gh % a.H;
   const int b = (gh / a.H) * G + gi;
   // BEAM: the shared path runs only when all 4 rows exist, route to a valid

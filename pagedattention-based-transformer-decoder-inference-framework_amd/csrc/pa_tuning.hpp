@@ -24,6 +24,7 @@ struct PaTuning {
   int beam_nsplit = 0;         // LLM_BEAM_NSPLIT: forced split count of beam-group launches
   int wgm_splits = 0;          // LLM_WGM_SPLITS: forced split count of workgroup-merge launches
   int beam4_splits = 0;        // LLM_BEAM4_SPLITS: forced split count of pa_beam4_kernel
+  bool beam_smaj = true;       // LLM_BEAM_SMAJ=0: beam workgroups in (group, head)-major order
 };
 
 // The steal form's exchange splits a shared page's 2 NI pieces of 1 KiB over

@@ -871,6 +871,7 @@ PaTuning pa_tuning() {
   t.beam_nsplit = env_int("LLM_BEAM_NSPLIT", 0);
   t.wgm_splits = env_int("LLM_WGM_SPLITS", 0);
   t.beam4_splits = env_int("LLM_BEAM4_SPLITS", 0);
+  t.beam_smaj = env_int("LLM_BEAM_SMAJ", 1) != 0;
   return t;
 }
 

@@ -99,12 +99,20 @@ def main():
     print("exit p90 per XCC:", [round(float(np.percentile(ex[xcc == x], 90)), 2)
                                 for x in range(8) if np.any(xcc == x)])
     # where the late waves are: by split, head, sequence (the grid's
-    # decomposition: wid = ((seq * H + head) * nsplit + split) * 4 + beam), and
+    # decomposition: wid = blk * 4 + beam, blk split-major unless LLM_BEAM_SMAJ=0), and
     # by how many waves their CU held
     H = cfg["H"]
-    split, rest = (wid // 4) % ns, (wid // 4) // ns
+    blk = wid // 4
+    if os.environ.get("LLM_BEAM_SMAJ", "1") != "0":  # split-major order (PaSplitArgs::smaj): blk = split * GH + seq * H + head
+        GH = ((B + 3) // 4) * H
+        split, rest = blk // GH, blk % GH
+    else:
+        split, rest = blk % ns, blk // ns
     head, seq = rest % H, rest // H
-    for name, key, k in (("split", split, ns), ("head", head, H), ("seq", seq, rest.max() + 1)):
+    nblk = ((B + 3) // 4) * H * ns
+    slot = blk * 4 // nblk  # dispatch slot: the CU's 1st..4th resident workgroup
+    for name, key, k in (("split", split, ns), ("head", head, H), ("seq", seq, rest.max() + 1),
+                         ("dispatch slot", slot, 4)):
         print(f"exit p50 / p90 by {name}:", " ".join(
             f"{int(i)}:{np.percentile(ex[key == i], 50):.1f}/{np.percentile(ex[key == i], 90):.1f}"
             for i in range(int(k)) if np.any(key == i)))

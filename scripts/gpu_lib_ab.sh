@@ -11,7 +11,7 @@ AB=${AB_DIR:-ab_old}
 mkdir -p $O
 for r in $(seq ${ROUNDS:-2}); do
   for c in ${CONFIGS:-c2 c4}; do
-    for v in old new; do
+    for v in ${ORDER:-old new}; do
       if [ $v = old ]; then LP=$R/$AB; else LP=; fi
       LD_LIBRARY_PATH=$LP${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} timeout -k 10 300 python bench.py --config $c --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline $EXTRA > $O/$c.$v.$r.json 2> $O/$c.$v.$r.err || { tail -5 $O/$c.$v.$r.err; exit 1; }
       python -c "import json;d=json.load(open('$O/$c.$v.$r.json'));r=d['roofline'];print('$c $v round $r', d['value'], d['ms_per_step'], r['launch_us'] if r else '')"
