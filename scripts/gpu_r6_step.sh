@@ -66,7 +66,7 @@ for s in ${STEPS:-tests smoke bench}; do
     tenv:*)  # tenv:<VAR>=<v>[+<VAR>=<v>...]:<config>: bench line on the TUNING build under those variables
       v=${s#tenv:}; kv=$(echo ${v%%:*} | tr + ' '); c=${v#*:}; tag=$(echo ${v%%:*} | tr -c 'A-Za-z0-9_\n' _)
       mkdir -p ab_tune && cp pagedattention-based-transformer-decoder-inference-framework_amd/libllm_decoder_hip_tune.so ab_tune/libllm_decoder_hip.so
-      env $kv LD_LIBRARY_PATH=$PWD/ab_tune${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} timeout -k 10 400 python bench.py --config $c --steps ${BSTEPS:-30} --warmup 5 --no-cpu-baseline > $O/tenv_${tag}_$c.json 2> $O/tenv_${tag}_$c.err || { tail -20 $O/tenv_${tag}_$c.err; exit 1; }
+      env $kv LD_LIBRARY_PATH=$PWD/ab_tune${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} timeout -k 10 400 python bench.py --config $c --steps ${BSTEPS:-30} --warmup 5 --no-cpu-baseline $BARGS > $O/tenv_${tag}_$c.json 2> $O/tenv_${tag}_$c.err || { tail -20 $O/tenv_${tag}_$c.err; exit 1; }
       python -c "import json;d=json.load(open('$O/tenv_${tag}_$c.json'));r=d['roofline'];print('tune [$kv] $c',d['value'],d['ms_per_step'],r.get('launch_us'))" ;;
     bench*)
       c=${s#bench}; c=${c:-c3}
