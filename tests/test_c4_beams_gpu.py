@@ -97,7 +97,8 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
     shared and private pages.  Oracle 1e-3, plain schedule 1e-5.  The same
     cases run through the tuning build's MFMA beam kernel (LLM_BEAM_MFMA=1),
     its one-wave-per-group kernel (LLM_BEAM4=1), the shipped form fed by an
-    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits), round 4's
+    LDS-DMA ring (LLM_BEAM_RING=3 / 4 / 8: the same bits), the group-major
+    workgroup order (LLM_BEAM_SMAJ=0: the same bits), round 4's
     contiguous cost-balanced splits (LLM_BEAM_INTERLEAVE=0) and the
     dynamic-assignment form (LLM_BEAM_STEAL=1)."""
     import torch
@@ -184,6 +185,15 @@ def test_beam_group_kernel_edges(gpu, oracle, B, T, shared, equal, monkeypatch):
                                   lib=llm_capi.load_tune()).cpu().numpy()
         assert np.array_equal(outr.view(np.uint32), outg.view(np.uint32)), (ring, rel_err(outr, outg))
     monkeypatch.delenv("LLM_BEAM_RING")
+    # ... and the group-major workgroup order (LLM_BEAM_SMAJ=0, the order until
+    # round 6; the product launches split-major): every workgroup does the same
+    # work either way, so the same bits
+    monkeypatch.setenv("LLM_BEAM_SMAJ", "0")
+    outo = llm_capi.pa_decode(d(q), d(kp), d(vp), d(pt), T=T, context_lens=d(lens),
+                              beam_ids=d(beam_ids), row_group=4,
+                              lib=llm_capi.load_tune()).cpu().numpy()
+    assert np.array_equal(outo.view(np.uint32), outg.view(np.uint32)), rel_err(outo, outg)
+    monkeypatch.delenv("LLM_BEAM_SMAJ")
     # ... and round 4's contiguous, cost-balanced splits (a 512-tile prefix scan
     # in every workgroup) in place of the interleaved ones
     monkeypatch.setenv("LLM_BEAM_INTERLEAVE", "0")
