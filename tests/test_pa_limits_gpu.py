@@ -1,4 +1,4 @@
-"""The paged attention launch at its size limits.
+"""The paged attention launch at its size limits, and the empty batch.
 
 The reference kernel has no bound of its own: it walks the page table for as
 many tiles as the call asks (attention/paged_flash_attention_kernel_fused.cu:27,
@@ -77,3 +77,22 @@ def test_one_page_past_the_limit_is_refused(gpu):
     out = llm_capi.pa_decode(q, kp, vp, pt, T=MAX_PAGES * ts - 5)
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
+
+
+def test_empty_batch_is_a_no_op(gpu):
+    """Zero rows (a decode step with no live sequence): attention (plain and
+    beam-group), the INT8 and FP16 GEMM entries return LLM_OK without a launch,
+    whatever their (NULL) operand pointers."""
+    import torch
+    import llm_capi
+    kp = torch.zeros((4, 16, 128), dtype=torch.float16, device="cuda")
+    pt = torch.zeros((1, 2, 4), dtype=torch.int32, device="cuda")
+    q = torch.zeros((0, 2, 128), dtype=torch.float32, device="cuda")
+    assert llm_capi.pa_decode(q, kp, kp, pt, T=64).shape == (0, 2, 128)
+    assert llm_capi.pa_decode(q, kp, kp, pt, T=64, row_group=4).shape == (0, 2, 128)
+    lib = llm_capi.load()
+    assert lib.i8_gemm(None, 256, None, None, None, 0, 64, 256, None, None, None, 0,
+                       llm_capi.stream_ptr()) == llm_capi.LLM_OK
+    assert lib.f16_gemm(None, 256, None, None, 0, 64, 256, None, 0,
+                        llm_capi.stream_ptr()) == llm_capi.LLM_OK
+    torch.cuda.synchronize()
