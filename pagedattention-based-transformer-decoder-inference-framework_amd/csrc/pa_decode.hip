@@ -717,8 +717,9 @@ int llm::pa_decode_internal(const pa_kv_view* kv, const float* q, int q_stride, 
   }
   a.balance16 = tn.beam_balance16;
   // beam-group workgroups in split-major order (PaSplitArgs::smaj).  Same box,
-  // C4 (profiles/r06/c4_smaj_ab.txt): 12,589 against 12,476 tok/s, launch
-  // 61.8 vs 62.9 us; the exits by dispatch slot stay 40 / 43.5 / 47 / 50 us
+  // C4 (profiles/r06/c4_smaj_ab.txt): 12,719-12,737 against 12,604-12,617
+  // tok/s; the launch's HBM bytes 1.031 -> 1.014x algorithmic
+  // (profiles/pmc_attention_c4.json), the exits by dispatch slot unchanged
   a.smaj = a.group == 4 && tn.beam_smaj ? 1 : 0;
   a.beam4 = use_beam4 ? 1 : 0;
   a.steal = a.group == 4 ? steal_ctr : nullptr;

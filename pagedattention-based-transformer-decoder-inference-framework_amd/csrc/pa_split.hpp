@@ -99,7 +99,8 @@ struct PaSplitArgs {
   // BEAM: split-major workgroup order (blockIdx = s * groups * H + group * H +
   // head) instead of ((group * H + head) * nsplit + s).  A CU's 4 resident
   // workgroups (blockIdx b, b + 256, b + 512, b + 768 at C4) are then 4 split
-  // pairs of 4 (group, head)s rather than 4 sequence pairs.
+  // pairs of 4 (group, head)s rather than 4 sequence pairs, and the splits of
+  // one (group, head) share an XCD (blockIdx mod 8) and its L2.
   int smaj;  // (last: the earlier fields keep their kernel-argument offsets)
 };
 
